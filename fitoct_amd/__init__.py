@@ -1,0 +1,11 @@
+"""fitoct_amd -- MI355X-native NUTS sampler for FitOCT's ExpGP posterior.
+
+Product path: Python (this package) -> ctypes -> libfitoct.so (C ABI,
+include/fitoct.h) -> HIP kernels for gfx950.  See DESIGN.md.
+"""
+from .api import (ExpGPProblem, Plan, SampleOutput, SamplerConfig, fitExpGP, logp_grad,
+                  sample)
+from ._lib import FitOCTError, lib
+
+__all__ = ["ExpGPProblem", "SamplerConfig", "Plan", "SampleOutput", "fitExpGP", "logp_grad",
+           "sample", "FitOCTError", "lib"]

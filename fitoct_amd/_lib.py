@@ -1,0 +1,148 @@
+"""ctypes binding of libfitoct.so (include/fitoct.h).
+
+This is the Python counterpart of the R ``.Call`` shim described in
+INTEGRATION.md: plain C structs, caller-owned numpy buffers, status codes
+turned into exceptions.  Loading fails loudly if the in-tree library is absent:
+there is no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfitoct.so")
+
+PRIOR = {"normal": 0, "lasso": 1, "horseshoe": 2}
+GRID = {"internal": 0, "extremal": 1}
+PREC = {"f64": 0, "mixed": 1}
+
+STATUS = {
+    0: "FITOCT_OK", -1: "FITOCT_E_ARG", -2: "FITOCT_E_HIP", -3: "FITOCT_E_NODEVICE",
+    -4: "FITOCT_E_INIT", -5: "FITOCT_E_NUMERIC", -6: "FITOCT_E_TIMEOUT", -7: "FITOCT_E_INTERNAL",
+}
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+class Problem(C.Structure):
+    _fields_ = [
+        ("N", C.c_int32), ("x", _dp), ("y", _dp), ("uy", _dp),
+        ("data_type", C.c_int32), ("Nn", C.c_int32), ("grid_type", C.c_int32),
+        ("rho", C.c_double), ("B", _dp),
+        ("theta0", C.c_double * 3), ("Sigma0", C.c_double * 9),
+        ("prior_type", C.c_int32), ("lambda_rate", C.c_double), ("lambda_scale", C.c_double),
+        ("nu", C.c_double), ("prior_PD", C.c_int32), ("kernel_conv", C.c_int32),
+        ("lambda_conv", C.c_int32), ("sigma_scale", C.c_double), ("nugget", C.c_double),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("chains", C.c_int32), ("chain_offset", C.c_int32), ("warmup", C.c_int32),
+        ("samples", C.c_int32), ("seed", C.c_uint64), ("adapt_delta", C.c_double),
+        ("max_treedepth", C.c_int32), ("adapt_engaged", C.c_int32), ("stepsize", C.c_double),
+        ("gamma", C.c_double), ("kappa", C.c_double), ("t0", C.c_double),
+        ("init_buffer", C.c_int32), ("term_buffer", C.c_int32), ("window", C.c_int32),
+        ("init_radius", C.c_double), ("save_warmup", C.c_int32), ("precision", C.c_int32),
+        ("device", C.c_int32),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [
+        ("draws", _dp), ("draws_capacity", C.c_int64), ("stepsize", _dp),
+        ("inv_metric", _dp), ("last_q", _dp), ("chain_status", _ip),
+        ("n_cols", C.c_int32), ("iters_saved", C.c_int32), ("dim", C.c_int32),
+        ("pad_", C.c_int32), ("total_leapfrogs", C.c_int64), ("kernel_ms", C.c_double),
+        ("wall_ms", C.c_double),
+    ]
+
+
+class PlanInfo(C.Structure):
+    _fields_ = [
+        ("dim", C.c_int32), ("n_cols", C.c_int32), ("iters_saved", C.c_int32),
+        ("chains", C.c_int32), ("tiles", C.c_int32), ("chains_per_tile", C.c_int32),
+        ("bins_per_thread", C.c_int32), ("threads_per_tile", C.c_int32),
+        ("lds_bytes", C.c_int32), ("n_pad", C.c_int32), ("draws_bytes", C.c_int64),
+    ]
+
+
+# every symbol declared in include/fitoct.h: (name, restype, argtypes)
+SIGNATURES = [
+    ("fitoct_abi_version", C.c_int32, []),
+    ("fitoct_last_error", C.c_char_p, []),
+    ("fitoct_device_count", C.c_int32, []),
+    ("fitoct_struct_sizes", C.c_int32, [_ip, _ip, _ip, _ip]),
+    ("fitoct_default_config", None, [C.POINTER(Config)]),
+    ("fitoct_default_problem", None, [C.POINTER(Problem)]),
+    ("fitoct_dim", C.c_int32, [C.c_int32, C.c_int32]),
+    ("fitoct_n_cols", C.c_int32, [C.c_int32, C.c_int32]),
+    ("fitoct_column_name", C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32]),
+    ("fitoct_build_basis", C.c_int32, [C.POINTER(Problem), _dp, _dp]),
+    ("fitoct_logp_grad", C.c_int32,
+     [C.POINTER(Problem), C.c_int32, _dp, _dp, _dp, _dp, C.c_int32, C.c_int32]),
+    ("fitoct_expgp_sample", C.c_int32, [C.POINTER(Problem), C.POINTER(Config), C.POINTER(Result)]),
+    ("fitoct_plan_create", C.c_int32,
+     [C.POINTER(Problem), C.POINTER(Config), C.POINTER(C.c_void_p)]),
+    ("fitoct_plan_get_info", C.c_int32, [C.c_void_p, C.POINTER(PlanInfo)]),
+    ("fitoct_plan_run", C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fitoct_plan_download", C.c_int32, [C.c_void_p, C.POINTER(Result)]),
+    ("fitoct_plan_destroy", None, [C.c_void_p]),
+    ("fitoct_split_rhat_ess", C.c_int32, [_dp, C.c_int32, C.c_int32, _dp, _dp]),
+    ("fitoct_rank_rhat", C.c_int32, [_dp, C.c_int32, C.c_int32, _dp]),
+]
+
+_LIB = None
+
+
+class FitOCTError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load the in-tree libfitoct.so (fails loudly if it was not built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} not found: build it with `python -m fitoct_amd.build` "
+                "(the HIP sampler has no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(code: int):
+    if code != 0:
+        raise FitOCTError(code, lib().fitoct_last_error().decode())
+
+
+def dptr(a: np.ndarray):
+    return a.ctypes.data_as(_dp) if a is not None else None
+
+
+def struct_sizes():
+    sz = [C.c_int32() for _ in range(4)]
+    lib().fitoct_struct_sizes(*[C.byref(s) for s in sz])
+    return tuple(s.value for s in sz)
+
+
+def column_names(prior_type: int, Nn: int):
+    L = lib()
+    n = L.fitoct_n_cols(prior_type, Nn)
+    buf = C.create_string_buffer(64)
+    out = []
+    for i in range(n):
+        check(L.fitoct_column_name(prior_type, Nn, i, buf, 64))
+        out.append(buf.value.decode())
+    return out

@@ -1,0 +1,288 @@
+"""Host-side mirror of FitOCTLib's ExpGP interface over the libfitoct C ABI.
+
+``fitExpGP`` keeps the R signature used by the reference's callers
+(FitOCT.R:110-124, priPost.R:2-16, ShinyInterface/server.R:408-426) -- same
+argument names, meanings and defaults -- and returns the same list shape
+``list(fit, method, xGP, prior_PD)`` (plotExpGP.R:29-32) as a dict whose ``fit``
+is a :class:`fitoct_amd.stanfit.StanFit` (print / extract / as_matrix / summary
+with Rhat and n_eff, as used at plotExpGP.R:7-50 and server.R:88-237).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import GRID, PREC, PRIOR, FitOCTError, check, dptr, lib
+
+
+@dataclass
+class ExpGPProblem:
+    """Inputs of one ExpGP fit (fields of ``fitoct_problem``)."""
+
+    x: np.ndarray
+    y: np.ndarray
+    uy: np.ndarray
+    dataType: int = 2
+    Nn: int = 10
+    gridType: str = "internal"
+    rho: float = 0.0                      # <= 0 -> 1/Nn
+    theta0: np.ndarray = field(default_factory=lambda: np.array([1000.0, 2000.0, 300.0]))
+    Sigma0: np.ndarray = None
+    prior_type: str = "normal"
+    lambda_rate: float = 0.1
+    lambda_scale: float = 10.0
+    nu: float = 1.0
+    prior_PD: int = 0
+    kernel_conv: int = 0
+    lambda_conv: int = 0
+    sigma_scale: float = 10.0
+    nugget: float = 1e-9
+    B: np.ndarray = None
+
+    def __post_init__(self):
+        self.x = np.ascontiguousarray(self.x, dtype=np.float64)
+        self.y = np.ascontiguousarray(self.y, dtype=np.float64)
+        self.uy = np.ascontiguousarray(self.uy, dtype=np.float64)
+        if not (self.x.shape == self.y.shape == self.uy.shape) or self.x.ndim != 1:
+            raise ValueError("x, y, uy must be 1-D arrays of equal length")
+        self.theta0 = np.ascontiguousarray(self.theta0, dtype=np.float64).reshape(3)
+        if self.Sigma0 is None:
+            self.Sigma0 = np.diag((0.05 * self.theta0) ** 2)
+        self.Sigma0 = np.ascontiguousarray(self.Sigma0, dtype=np.float64).reshape(3, 3)
+        if self.B is not None:
+            self.B = np.ascontiguousarray(self.B, dtype=np.float64).reshape(self.x.size, self.Nn)
+        if self.gridType not in GRID:
+            raise ValueError(f"gridType must be one of {list(GRID)}")
+        if self.prior_type not in PRIOR:
+            raise ValueError(f"prior_type must be one of {list(PRIOR)}")
+
+    @property
+    def N(self) -> int:
+        return self.x.size
+
+    @property
+    def family(self) -> int:
+        return PRIOR[self.prior_type]
+
+    @property
+    def D(self) -> int:
+        return lib().fitoct_dim(self.family, self.Nn)
+
+    def to_c(self) -> _lib.Problem:
+        p = _lib.Problem()
+        p.N = self.N
+        p.x, p.y, p.uy = dptr(self.x), dptr(self.y), dptr(self.uy)
+        p.data_type = int(self.dataType)
+        p.Nn = int(self.Nn)
+        p.grid_type = GRID[self.gridType]
+        p.rho = float(self.rho if self.rho else 0.0)
+        p.B = dptr(self.B) if self.B is not None else None
+        p.theta0[:] = list(self.theta0)
+        p.Sigma0[:] = list(self.Sigma0.ravel())
+        p.prior_type = self.family
+        p.lambda_rate = float(self.lambda_rate)
+        p.lambda_scale = float(self.lambda_scale)
+        p.nu = float(self.nu)
+        p.prior_PD = int(self.prior_PD)
+        p.kernel_conv = int(self.kernel_conv)
+        p.lambda_conv = int(self.lambda_conv)
+        p.sigma_scale = float(self.sigma_scale)
+        p.nugget = float(self.nugget)
+        return p
+
+    def basis(self):
+        """(B[N, Nn], xGP[Nn]) as built by the library (fp64 Cholesky, host)."""
+        B = np.zeros((self.N, self.Nn))
+        xg = np.zeros(self.Nn)
+        p = self.to_c()
+        check(lib().fitoct_build_basis(C.byref(p), dptr(B), dptr(xg)))
+        return B, xg
+
+    def column_names(self):
+        return _lib.column_names(self.family, self.Nn)
+
+
+@dataclass
+class SamplerConfig:
+    """``rstan::sampling`` controls (testGamma.R:42-47) + sharding."""
+
+    chains: int = 4
+    warmup: int = 500
+    samples: int = 1000
+    seed: int = 1234
+    adapt_delta: float = 0.8
+    max_treedepth: int = 10
+    adapt_engaged: bool = True
+    stepsize: float = 1.0
+    gamma: float = 0.05
+    kappa: float = 0.75
+    t0: float = 10.0
+    init_buffer: int = 75
+    term_buffer: int = 50
+    window: int = 25
+    init_radius: float = 2.0
+    save_warmup: bool = True
+    precision: str = "f64"
+    device: int = 0
+    chain_offset: int = 0
+
+    def to_c(self) -> _lib.Config:
+        c = _lib.Config()
+        c.chains = int(self.chains)
+        c.chain_offset = int(self.chain_offset)
+        c.warmup = int(self.warmup)
+        c.samples = int(self.samples)
+        c.seed = int(self.seed) & 0xFFFFFFFFFFFFFFFF
+        c.adapt_delta = float(self.adapt_delta)
+        c.max_treedepth = int(self.max_treedepth)
+        c.adapt_engaged = 1 if self.adapt_engaged else 0
+        c.stepsize = float(self.stepsize)
+        c.gamma, c.kappa, c.t0 = float(self.gamma), float(self.kappa), float(self.t0)
+        c.init_buffer, c.term_buffer, c.window = (int(self.init_buffer), int(self.term_buffer),
+                                                  int(self.window))
+        c.init_radius = float(self.init_radius)
+        c.save_warmup = 1 if self.save_warmup else 0
+        c.precision = PREC[self.precision]
+        c.device = int(self.device)
+        return c
+
+
+def logp_grad(prob: ExpGPProblem, q: np.ndarray, precision: str = "f64", device: int = 0):
+    """Batched log density / gradient on the GPU: q[P, D] -> (lp[P], grad[P, D], sumr2[P])."""
+    q = np.ascontiguousarray(np.atleast_2d(q), dtype=np.float64)
+    P, D = q.shape
+    if D != prob.D:
+        raise ValueError(f"q has {D} columns, model dimension is {prob.D}")
+    lp = np.zeros(P)
+    g = np.zeros((P, D))
+    s2 = np.zeros(P)
+    p = prob.to_c()
+    check(lib().fitoct_logp_grad(C.byref(p), P, dptr(q), dptr(lp), dptr(g), dptr(s2),
+                                 PREC[precision], device))
+    return lp, g, s2
+
+
+@dataclass
+class SampleOutput:
+    draws: np.ndarray          # [chains, iters_saved, n_cols]
+    columns: list
+    warmup_saved: int          # leading warmup iterations included in draws
+    stepsize: np.ndarray
+    inv_metric: np.ndarray
+    last_q: np.ndarray
+    total_leapfrogs: int
+    kernel_ms: float
+    wall_ms: float
+    chain_offset: int = 0
+
+
+class Plan:
+    """A planned sampler run: inputs staged in HBM once, run many times."""
+
+    def __init__(self, prob: ExpGPProblem, cfg: SamplerConfig):
+        self.prob, self.cfg = prob, cfg
+        self._p = prob.to_c()
+        self._c = cfg.to_c()
+        h = C.c_void_p()
+        check(lib().fitoct_plan_create(C.byref(self._p), C.byref(self._c), C.byref(h)))
+        self._h = h
+        info = _lib.PlanInfo()
+        check(lib().fitoct_plan_get_info(self._h, C.byref(info)))
+        self.info = {f: getattr(info, f) for f, _ in _lib.PlanInfo._fields_}
+
+    def run(self, d_draws: int = 0, stream: int = 0):
+        """Run on ``stream`` (hipStream_t as int); draws to the device buffer
+        ``d_draws`` (int pointer, >= info['draws_bytes']) or a plan-internal one."""
+        check(lib().fitoct_plan_run(self._h, C.c_void_p(d_draws or None),
+                                    C.c_void_p(stream or None)))
+
+    def download(self) -> SampleOutput:
+        i = self.info
+        C_, D = i["chains"], i["dim"]
+        draws = np.empty((C_, i["iters_saved"], i["n_cols"]))
+        eps = np.empty(C_)
+        minv = np.empty((C_, D))
+        lq = np.empty((C_, D))
+        st = np.zeros(C_, dtype=np.int32)
+        r = _lib.Result()
+        r.draws = dptr(draws)
+        r.draws_capacity = draws.size
+        r.stepsize, r.inv_metric, r.last_q = dptr(eps), dptr(minv), dptr(lq)
+        r.chain_status = st.ctypes.data_as(C.POINTER(C.c_int32))
+        check(lib().fitoct_plan_download(self._h, C.byref(r)))
+        return SampleOutput(draws, self.prob.column_names(),
+                            self.cfg.warmup if self.cfg.save_warmup else 0, eps, minv, lq,
+                            int(r.total_leapfrogs), float(r.kernel_ms), 0.0,
+                            self.cfg.chain_offset)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().fitoct_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def sample(prob: ExpGPProblem, cfg: SamplerConfig) -> SampleOutput:
+    """One-shot sampler run (plan + run + download)."""
+    t0 = time.perf_counter()
+    with Plan(prob, cfg) as pl:
+        pl.run()
+        out = pl.download()
+    out.wall_ms = (time.perf_counter() - t0) * 1e3
+    return out
+
+
+# --------------------------------------------------------------------------
+# FitOCTLib-compatible entry point
+# --------------------------------------------------------------------------
+def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
+             theta0=None, Sigma0=None, lambda_rate=0.1, rho_scale=0.0, nb_warmup=500,
+             nb_iter=1000, prior_PD=0, open_progress=False, *, nb_chains=4,
+             prior_type="normal", lambda_scale=10.0, nu=1.0, adapt_delta=0.8,
+             max_treedepth=10, seed=None, precision="f64", device=0, **model_switches):
+    """Drop-in for ``FitOCTLib::fitExpGP`` (FitOCT.R:110-124).
+
+    ``nb_iter`` counts warmup + sampling iterations, as the callers pass
+    ``nb_iter = nb_warmup + nb_sample`` (FitOCT.R:121).  ``rho_scale`` <= 0 means
+    ``1/Nn`` (FitOCT.R:119).  Only ``method='sample'`` runs on the GPU; 'optim'
+    and 'vb' are SURVEY §8f rank-3 rows and raise NotImplementedError here.
+    Returns ``dict(fit, method, xGP, prior_PD, lasso)``.
+    """
+    from .stanfit import StanFit
+
+    if method != "sample":
+        raise NotImplementedError(f"method={method!r}: only 'sample' is on the HIP path")
+    if theta0 is None:
+        raise ValueError("theta0 is required (FitOCTLib::estimateExpPrior output)")
+    nb_sample = int(nb_iter) - int(nb_warmup)
+    if nb_sample < 1:
+        raise ValueError("nb_iter must exceed nb_warmup")
+    prob = ExpGPProblem(x, y, uy, dataType=dataType, Nn=Nn, gridType=gridType,
+                        rho=rho_scale if rho_scale and rho_scale > 0 else 0.0, theta0=theta0,
+                        Sigma0=Sigma0, prior_type=prior_type, lambda_rate=lambda_rate,
+                        lambda_scale=lambda_scale, nu=nu, prior_PD=prior_PD, **model_switches)
+    if seed is None:
+        seed = int(np.random.SeedSequence().entropy & 0xFFFFFFFF)
+    cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_sample, seed=seed,
+                        adapt_delta=adapt_delta, max_treedepth=max_treedepth,
+                        precision=precision, device=device)
+    out = sample(prob, cfg)
+    _, xGP = prob.basis()
+    fit = StanFit.from_output(out, prob)
+    return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,
+            "lasso": prior_type == "lasso"}

@@ -1,0 +1,80 @@
+"""Build libfitoct.so in-tree (hipcc, gfx950).  No torch, no JIT cache: the
+shared object sits next to this file so it travels with the repository
+snapshot to the GPU box.
+
+    python -m fitoct_amd.build [--force] [--verbose]
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+LIB = os.path.join(HERE, "libfitoct.so")
+OBJDIR = os.path.join(HERE, "build")
+ARCH = os.environ.get("FITOCT_ARCH", "gfx950")
+
+SOURCES = [
+    # (source, compiler, flags)
+    ("nuts_device.hip", "hipcc", [f"--offload-arch={ARCH}", "-O3", "-std=c++17"]),
+    ("fitoct_api.cpp", "hipcc", [f"--offload-arch={ARCH}", "-O2", "-std=c++17"]),
+    ("host_model.cpp", "g++", ["-O2", "-std=c++17"]),
+]
+HEADERS = ["kernel_params.h", "philox.h", "host_internal.h"]
+
+
+def _hipcc() -> str:
+    for c in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm required to build libfitoct)")
+
+
+def _newest_input() -> float:
+    paths = [os.path.join(CSRC, s) for s, _, _ in SOURCES]
+    paths += [os.path.join(CSRC, h) for h in HEADERS]
+    paths += [os.path.join(INCLUDE, "fitoct.h"), os.path.abspath(__file__)]
+    return max(os.path.getmtime(p) for p in paths)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every translation unit and link ``fitoct_amd/libfitoct.so``."""
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_input():
+        return LIB
+    os.makedirs(OBJDIR, exist_ok=True)
+    hipcc = _hipcc()
+
+    def compile_one(item):
+        src, cc, flags = item
+        obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+        exe = hipcc if cc == "hipcc" else (shutil.which("g++") or "g++")
+        cmd = [exe, *flags, "-fPIC", "-Wall", f"-I{INCLUDE}", f"-I{CSRC}",
+               "-I/opt/rocm/include", "-c", os.path.join(CSRC, src), "-o", obj]
+        if cc != "hipcc":
+            cmd.insert(1, "-D__HIP_PLATFORM_AMD__")
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        if verbose and r.stderr.strip():
+            print(r.stderr, file=sys.stderr)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = LIB + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose="--verbose" in sys.argv))

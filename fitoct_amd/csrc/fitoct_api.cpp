@@ -1,0 +1,609 @@
+// C ABI of libfitoct (include/fitoct.h): argument checking, device planning,
+// data staging in HBM, kernel dispatch and result download.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <stdlib.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "fitoct.h"
+#include "host_internal.h"
+#include "kernel_params.h"
+
+namespace fitoct {
+hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P, int tiles,
+                  hipStream_t st);
+int lds_bytes(int ppl, int G);
+}  // namespace fitoct
+
+using namespace fitoct;
+
+#define HIP_TRY(expr)                                                                 \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(FITOCT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+  } while (0)
+
+struct fitoct_plan {
+  fitoct_problem prob{};
+  fitoct_config cfg{};
+  KParams kp{};
+  int tiles = 0, bpt = 0, nnp = 16, ppl = 1, lds = 0;
+  bool mixed = false;
+  size_t draws_bytes = 0;
+  void* d_data = nullptr;     // cx | y | isu | B  (type R)
+  double* d_draws = nullptr;  // internal draws buffer (lazily allocated)
+  double* d_stack = nullptr;
+  double* d_fin = nullptr;    // eps[C] | minv[C*D] | q[C*D]
+  int* d_status = nullptr;
+  long long* d_leap = nullptr;
+  double* last_draws = nullptr;
+  double kernel_ms = 0.0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool ran = false;
+};
+
+namespace {
+
+int check_problem(const fitoct_problem* p) {
+  if (!p) return fail(FITOCT_E_ARG, "problem is NULL");
+  if (p->N < 2) return fail(FITOCT_E_ARG, "N must be >= 2");
+  if (!p->x || !p->y || !p->uy) return fail(FITOCT_E_ARG, "x, y, uy must be non-NULL");
+  if (p->Nn < 2 || p->Nn > 24) return fail(FITOCT_E_ARG, "Nn must be in [2, 24]");
+  if (model_dim(p->prior_type, p->Nn) < 0) return fail(FITOCT_E_ARG, "unknown prior_type");
+  if (p->data_type != 1 && p->data_type != 2) return fail(FITOCT_E_ARG, "data_type must be 1 or 2");
+  for (int i = 0; i < p->N; ++i) {
+    if (!isfinite(p->x[i]) || !isfinite(p->y[i]) || !(p->uy[i] > 0.0) || !isfinite(p->uy[i]))
+      return fail(FITOCT_E_ARG, "x, y must be finite and uy > 0 at bin " + std::to_string(i));
+  }
+  for (int j = 0; j < 3; ++j)
+    if (!(p->theta0[j] > 0.0)) return fail(FITOCT_E_ARG, "theta0 must be > 0");
+  if (p->prior_type == FITOCT_PRIOR_NORMAL && !(p->lambda_rate > 0.0))
+    return fail(FITOCT_E_ARG, "lambda_rate must be > 0");
+  if (p->prior_type == FITOCT_PRIOR_LASSO && !(p->lambda_scale > 0.0))
+    return fail(FITOCT_E_ARG, "lambda_scale must be > 0");
+  if (p->prior_type == FITOCT_PRIOR_HORSESHOE && !(p->nu >= 1.0))
+    return fail(FITOCT_E_ARG, "nu must be >= 1 (horseShoePrior.stan:13)");
+  if (!(p->sigma_scale > 0.0)) return fail(FITOCT_E_ARG, "sigma_scale must be > 0");
+  return FITOCT_OK;
+}
+
+int invert3(const double* S, double* Si) {
+  const double a = S[0], b = S[1], c = S[2], d = S[3], e = S[4], f = S[5], g = S[6], h = S[7],
+               i = S[8];
+  const double A = e * i - f * h, B = -(d * i - f * g), C = d * h - e * g;
+  const double det = a * A + b * B + c * C;
+  if (!(fabs(det) > 0.0) || !isfinite(det)) return fail(FITOCT_E_ARG, "Sigma0 is singular");
+  Si[0] = A / det;
+  Si[1] = -(b * i - c * h) / det;
+  Si[2] = (b * f - c * e) / det;
+  Si[3] = B / det;
+  Si[4] = (a * i - c * g) / det;
+  Si[5] = -(a * f - c * d) / det;
+  Si[6] = C / det;
+  Si[7] = -(a * h - b * g) / det;
+  Si[8] = (a * e - b * d) / det;
+  if (!(A > 0.0) || !(det > 0.0)) return fail(FITOCT_E_ARG, "Sigma0 must be positive definite");
+  return FITOCT_OK;
+}
+
+// Shapes: bins are strided over the 1024 lanes of a tile; up to 4 bins per lane
+// keep their data in registers (MODE_POLY: 5 values per bin; MODE_BREG: 3 + NNP
+// fp32 values, up to 2 bins), beyond that the basis rows are streamed.
+void choose_bins(int N, int& bpt, int& n_pad) {
+  if (N <= TPB) { bpt = 1; n_pad = TPB; }
+  else if (N <= 2 * TPB) { bpt = 2; n_pad = 2 * TPB; }
+  else if (N <= 4 * TPB) { bpt = 4; n_pad = 4 * TPB; }
+  else { bpt = 0; n_pad = (N + TPB - 1) / TPB * TPB; }
+}
+
+// MODE_POLY factors of the SE basis on the uniform grid g_l = g_0 + l*dg:
+//   K(x~_i, g_l) = a_i t_i^l b_l, a_i = exp(-(x~_i-g_0)^2/(2s2)),
+//   t_i = exp((x~_i-g_0) dg/s2), b_l = exp(-(l dg)^2/(2s2)),
+// and K^-1 = (K(xGP,xGP) + nugget I)^-1.  Accepted only if the factorised basis
+// reproduces the Cholesky basis B to 1e-10 (relative to max|B|) and no power
+// t^l (l < nnp) can overflow; otherwise the caller falls back to streamed rows.
+bool build_poly(const fitoct_problem* p, const std::vector<double>& B, int nnp,
+                std::vector<double>& ta, std::vector<double>& kinv, std::vector<double>& bv) {
+  const int N = p->N, Nn = p->Nn;
+  double xmin = p->x[0], xmax = p->x[0];
+  for (int i = 1; i < N; ++i) {
+    xmin = std::min(xmin, p->x[i]);
+    xmax = std::max(xmax, p->x[i]);
+  }
+  const double rho = (p->rho > 0.0) ? p->rho : 1.0 / Nn;
+  const double s2 = (p->kernel_conv == 0) ? rho * rho : 0.5 * rho * rho;
+  double g0, dg;
+  if (p->grid_type == FITOCT_GRID_INTERNAL) {
+    const double dx = 1.0 / (Nn + 1);
+    g0 = dx / 2;
+    dg = (1.0 - dx) / (Nn - 1);
+  } else {
+    g0 = 0.0;
+    dg = 1.0 / (Nn - 1);
+  }
+  ta.assign((size_t)2 * N, 0.0);
+  for (int i = 0; i < N; ++i) {
+    const double u = (p->x[i] - xmin) / (xmax - xmin) - g0;
+    const double lt = u * dg / s2, la = -u * u / (2.0 * s2);
+    if (fabs(lt) * (nnp - 1) > 650.0 || la < -650.0) return false;
+    ta[2 * i] = exp(lt);
+    ta[2 * i + 1] = exp(la);
+  }
+  bv.assign(Nn, 0.0);
+  for (int l = 0; l < Nn; ++l) bv[l] = exp(-(l * dg) * (l * dg) / (2.0 * s2));
+  // K^-1 by Cholesky
+  std::vector<double> xg(Nn), L((size_t)Nn * Nn, 0.0);
+  for (int k = 0; k < Nn; ++k) xg[k] = g0 + k * dg;
+  for (int i = 0; i < Nn; ++i)
+    for (int j = 0; j <= i; ++j) {
+      const double d = xg[i] - xg[j];
+      double sum = exp(-d * d / (2.0 * s2)) + (i == j ? p->nugget : 0.0);
+      for (int k = 0; k < j; ++k) sum -= L[i * Nn + k] * L[j * Nn + k];
+      if (i == j) {
+        if (!(sum > 0.0)) return false;
+        L[i * Nn + i] = sqrt(sum);
+      } else {
+        L[i * Nn + j] = sum / L[j * Nn + j];
+      }
+    }
+  std::vector<double> Li((size_t)Nn * Nn, 0.0);  // L^-1 (lower)
+  for (int j = 0; j < Nn; ++j) {
+    Li[j * Nn + j] = 1.0 / L[j * Nn + j];
+    for (int i = j + 1; i < Nn; ++i) {
+      double sum = 0.0;
+      for (int k = j; k < i; ++k) sum -= L[i * Nn + k] * Li[k * Nn + j];
+      Li[i * Nn + j] = sum / L[i * Nn + i];
+    }
+  }
+  kinv.assign((size_t)Nn * Nn, 0.0);
+  for (int i = 0; i < Nn; ++i)
+    for (int j = 0; j < Nn; ++j) {
+      double sum = 0.0;
+      for (int k = std::max(i, j); k < Nn; ++k) sum += Li[k * Nn + i] * Li[k * Nn + j];
+      kinv[i * Nn + j] = sum;
+    }
+  // exactness check against the Cholesky basis
+  double bmax = 0.0, err = 0.0;
+  std::vector<double> row(Nn);
+  for (int i = 0; i < N; ++i) {
+    double tp = ta[2 * i + 1];
+    for (int l = 0; l < Nn; ++l) {
+      row[l] = tp * bv[l];
+      tp *= ta[2 * i];
+    }
+    for (int k = 0; k < Nn; ++k) {
+      double v = 0.0;
+      for (int l = 0; l < Nn; ++l) v += row[l] * kinv[l * Nn + k];
+      const double b = B[(size_t)i * Nn + k];
+      bmax = std::max(bmax, fabs(b));
+      err = std::max(err, fabs(v - b));
+    }
+  }
+  return err <= 1e-10 * std::max(1.0, bmax);
+}
+
+template <class R>
+void stage(const fitoct_problem* p, const std::vector<double>& B, const std::vector<double>& ta,
+           int mode, int n_pad, int nnp, std::vector<char>& out) {
+  const size_t n = (size_t)n_pad;
+  const int nr = (mode == MODE_POLY) ? 2 : nnp;
+  out.assign(sizeof(R) * (3 * n + n * nr), 0);
+  R* cx = (R*)out.data();
+  R* y = cx + n;
+  R* isu = y + n;
+  R* Bp = isu + n;
+  for (int i = 0; i < p->N; ++i) {
+    cx[i] = (R)((double)p->data_type * p->x[i]);
+    y[i] = (R)p->y[i];
+    isu[i] = (R)(1.0 / p->uy[i]);
+    if (mode == MODE_POLY) {
+      Bp[2 * (size_t)i] = (R)ta[2 * (size_t)i];
+      Bp[2 * (size_t)i + 1] = (R)ta[2 * (size_t)i + 1];
+    } else {
+      for (int k = 0; k < p->Nn; ++k) Bp[(size_t)i * nnp + k] = (R)B[(size_t)i * p->Nn + k];
+    }
+  }
+}
+
+// common planning for the sampler and the logp kernel
+int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precision, int device) {
+  int rc = check_problem(p);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(FITOCT_E_NODEVICE, "no HIP device visible");
+  if (device < 0 || device >= ndev) return fail(FITOCT_E_ARG, "device ordinal out of range");
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+
+  pl->prob = *p;
+  pl->prob.x = pl->prob.y = pl->prob.uy = pl->prob.B = nullptr;  // never keep caller pointers
+  pl->mixed = (precision == FITOCT_PREC_MIXED);
+  const int D = model_dim(p->prior_type, p->Nn);
+  pl->nnp = (p->Nn <= 16) ? 16 : 24;
+  pl->ppl = (D <= WAVE) ? 1 : 2;
+  if (pl->nnp == 16 && pl->ppl == 2) pl->nnp = 24;  // the (24, 2) instantiation covers it
+  if (pl->nnp == 24) pl->ppl = 2;
+  int n_pad;
+  choose_bins(p->N, pl->bpt, n_pad);
+
+  std::vector<double> B, xg;
+  if (p->B) {
+    B.assign(p->B, p->B + (size_t)p->N * p->Nn);
+  } else {
+    rc = build_basis(p, B, xg);
+    if (rc) return rc;
+  }
+  // basis mode (see kernel_params.h BasisMode)
+  std::vector<double> ta, kinv, bv;
+  int mode;
+  if (pl->mixed) {
+    mode = (pl->bpt == 1 || pl->bpt == 2) ? MODE_BREG : MODE_STREAM;
+  } else {
+    const bool poly = !p->B && pl->bpt > 0 && getenv("FITOCT_NO_POLY") == nullptr &&
+                      build_poly(p, B, pl->nnp, ta, kinv, bv);
+    mode = poly ? MODE_POLY : MODE_STREAM;
+  }
+  if (mode == MODE_STREAM) pl->bpt = 0;
+  std::vector<char> staged;
+  if (pl->mixed) stage<float>(p, B, ta, mode, n_pad, pl->nnp, staged);
+  else stage<double>(p, B, ta, mode, n_pad, pl->nnp, staged);
+  const size_t kbytes = sizeof(double) * (kinv.size() + bv.size());
+  HIP_TRY(hipMalloc(&pl->d_data, staged.size() + kbytes + 16));
+  HIP_TRY(hipMemcpy(pl->d_data, staged.data(), staged.size(), hipMemcpyHostToDevice));
+  double* dk = (double*)((char*)pl->d_data + (staged.size() + 15) / 16 * 16);
+  if (mode == MODE_POLY) {
+    HIP_TRY(hipMemcpy(dk, kinv.data(), sizeof(double) * kinv.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dk + kinv.size(), bv.data(), sizeof(double) * bv.size(),
+                      hipMemcpyHostToDevice));
+  }
+  const size_t rs = pl->mixed ? sizeof(float) : sizeof(double);
+  KParams& k = pl->kp;
+  k.cx = pl->d_data;
+  k.y = (const char*)pl->d_data + rs * n_pad;
+  k.isu = (const char*)pl->d_data + 2 * rs * n_pad;
+  k.B = (const char*)pl->d_data + 3 * rs * n_pad;
+  k.mode = mode;
+  k.Kinv = dk;
+  k.bvec = dk + kinv.size();
+  k.N = p->N;
+  k.n_pad = n_pad;
+  k.Nn = p->Nn;
+  k.D = D;
+  k.family = p->prior_type;
+  k.prior_PD = p->prior_PD ? 1 : 0;
+  for (int j = 0; j < 3; ++j) k.theta0[j] = p->theta0[j];
+  rc = invert3(p->Sigma0, k.S0inv);
+  if (rc) return rc;
+  k.lambda_rate_eff = (p->lambda_conv == 0) ? 1.0 / p->lambda_rate : p->lambda_rate;
+  k.lambda_scale = p->lambda_scale;
+  k.nu = p->nu;
+  k.sigma_scale = p->sigma_scale;
+  k.chains = chains;
+
+  // chains per tile: fill every CU with one tile first, then stack chains
+  const int ncu = std::max(1, prop.multiProcessorCount);
+  int G = std::max(1, std::min(GMAX, (chains + ncu - 1) / ncu));
+  while (G > 1 && lds_bytes(pl->ppl, G) > 160 * 1024 - 256) --G;
+  k.G = G;
+  pl->tiles = (chains + G - 1) / G;
+  pl->lds = lds_bytes(pl->ppl, G);
+  return FITOCT_OK;
+}
+
+void free_plan(fitoct_plan* pl) {
+  if (!pl) return;
+  (void)hipFree(pl->d_data);
+  (void)hipFree(pl->d_draws);
+  (void)hipFree(pl->d_stack);
+  (void)hipFree(pl->d_fin);
+  (void)hipFree(pl->d_status);
+  (void)hipFree(pl->d_leap);
+  if (pl->ev0) (void)hipEventDestroy(pl->ev0);
+  if (pl->ev1) (void)hipEventDestroy(pl->ev1);
+  delete pl;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t fitoct_abi_version(void) { return FITOCT_ABI_VERSION; }
+
+const char* fitoct_last_error(void) { return g_last_error.c_str(); }
+
+int32_t fitoct_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int32_t fitoct_struct_sizes(int32_t* problem, int32_t* config, int32_t* result, int32_t* info) {
+  if (problem) *problem = (int32_t)sizeof(fitoct_problem);
+  if (config) *config = (int32_t)sizeof(fitoct_config);
+  if (result) *result = (int32_t)sizeof(fitoct_result);
+  if (info) *info = (int32_t)sizeof(fitoct_plan_info);
+  return FITOCT_OK;
+}
+
+void fitoct_default_config(fitoct_config* c) {
+  if (!c) return;
+  memset(c, 0, sizeof *c);
+  c->chains = 4;  // server.R:469
+  c->warmup = 500;
+  c->samples = 1000;
+  c->seed = 1234;
+  c->adapt_delta = 0.8;
+  c->max_treedepth = 10;
+  c->adapt_engaged = 1;
+  c->stepsize = 1.0;
+  c->gamma = 0.05;
+  c->kappa = 0.75;
+  c->t0 = 10.0;
+  c->init_buffer = 75;
+  c->term_buffer = 50;
+  c->window = 25;
+  c->init_radius = 2.0;
+  c->save_warmup = 1;
+  c->precision = FITOCT_PREC_F64;
+}
+
+void fitoct_default_problem(fitoct_problem* p) {
+  if (!p) return;
+  memset(p, 0, sizeof *p);
+  p->data_type = 2;
+  p->Nn = 10;
+  p->grid_type = FITOCT_GRID_INTERNAL;
+  p->prior_type = FITOCT_PRIOR_NORMAL;
+  p->lambda_rate = 0.1;
+  p->lambda_scale = 10.0;
+  p->nu = 1.0;
+  p->sigma_scale = 10.0;
+  p->nugget = 1e-9;
+  p->theta0[0] = 1000.0;
+  p->theta0[1] = 2000.0;
+  p->theta0[2] = 300.0;
+  for (int j = 0; j < 3; ++j) p->Sigma0[4 * j] = (0.05 * p->theta0[j]) * (0.05 * p->theta0[j]);
+}
+
+int32_t fitoct_dim(int32_t prior_type, int32_t Nn) { return model_dim(prior_type, Nn); }
+
+int32_t fitoct_n_cols(int32_t prior_type, int32_t Nn) {
+  const int D = model_dim(prior_type, Nn);
+  return D < 0 ? -1 : D + 8;
+}
+
+int32_t fitoct_column_name(int32_t prior_type, int32_t Nn, int32_t i, char* buf, int32_t buflen) {
+  const std::string s = column_name(prior_type, Nn, i);
+  if (s.empty()) return fail(FITOCT_E_ARG, "column index out of range");
+  if (!buf || buflen < (int32_t)s.size() + 1) return fail(FITOCT_E_ARG, "buffer too small");
+  memcpy(buf, s.c_str(), s.size() + 1);
+  return FITOCT_OK;
+}
+
+int32_t fitoct_build_basis(const fitoct_problem* prob, double* B_out, double* xGP_out) {
+  if (!prob || !B_out) return fail(FITOCT_E_ARG, "NULL argument");
+  if (prob->N < 2 || !prob->x) return fail(FITOCT_E_ARG, "need x with N >= 2");
+  std::vector<double> B, xg;
+  const int rc = build_basis(prob, B, xg);
+  if (rc) return rc;
+  memcpy(B_out, B.data(), B.size() * sizeof(double));
+  if (xGP_out) memcpy(xGP_out, xg.data(), xg.size() * sizeof(double));
+  return FITOCT_OK;
+}
+
+int32_t fitoct_logp_grad(const fitoct_problem* prob, int32_t n_points, const double* q,
+                         double* lp_out, double* grad_out, double* sumr2_out, int32_t precision,
+                         int32_t device) {
+  if (n_points < 1 || !q || !lp_out || !grad_out) return fail(FITOCT_E_ARG, "bad buffers");
+  fitoct_plan* pl = new fitoct_plan();
+  int rc = plan_common(pl, prob, n_points, precision, device);
+  if (rc) {
+    free_plan(pl);
+    return rc;
+  }
+  KParams k = pl->kp;
+  const int D = k.D;
+  double *d_q = nullptr, *d_out = nullptr;
+  auto run = [&]() -> int {
+    HIP_TRY(hipMalloc(&d_q, sizeof(double) * (size_t)n_points * D));
+    HIP_TRY(hipMalloc(&d_out, sizeof(double) * (size_t)n_points * (D + 2)));
+    HIP_TRY(hipMemcpy(d_q, q, sizeof(double) * (size_t)n_points * D, hipMemcpyHostToDevice));
+    k.q_in = d_q;
+    k.grad_out = d_out;
+    k.lp_out = d_out + (size_t)n_points * D;
+    k.s2_out = k.lp_out + n_points;
+    HIP_TRY(launch(true, pl->mixed, pl->bpt, pl->nnp, k, pl->tiles, 0));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(grad_out, d_out, sizeof(double) * (size_t)n_points * D, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(lp_out, k.lp_out, sizeof(double) * n_points, hipMemcpyDeviceToHost));
+    if (sumr2_out)
+      HIP_TRY(hipMemcpy(sumr2_out, k.s2_out, sizeof(double) * n_points, hipMemcpyDeviceToHost));
+    return FITOCT_OK;
+  };
+  rc = run();
+  (void)hipFree(d_q);
+  (void)hipFree(d_out);
+  free_plan(pl);
+  return rc;
+}
+
+int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
+                           fitoct_plan** out) {
+  if (!out) return fail(FITOCT_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (!cfg) return fail(FITOCT_E_ARG, "config is NULL");
+  if (cfg->chains < 1) return fail(FITOCT_E_ARG, "chains must be >= 1");
+  if (cfg->warmup < 0 || cfg->samples < 1) return fail(FITOCT_E_ARG, "warmup >= 0, samples >= 1");
+  if (cfg->max_treedepth < 1 || cfg->max_treedepth > MAXDEPTH)
+    return fail(FITOCT_E_ARG, "max_treedepth must be in [1, 16]");
+  if (!(cfg->adapt_delta > 0.0 && cfg->adapt_delta < 1.0))
+    return fail(FITOCT_E_ARG, "adapt_delta must be in (0, 1)");
+  if (!(cfg->stepsize > 0.0)) return fail(FITOCT_E_ARG, "stepsize must be > 0");
+  fitoct_plan* pl = new fitoct_plan();
+  int rc = plan_common(pl, prob, cfg->chains, cfg->precision, cfg->device);
+  if (rc) {
+    free_plan(pl);
+    return rc;
+  }
+  pl->cfg = *cfg;
+  KParams& k = pl->kp;
+  const int C = cfg->chains, D = k.D;
+  k.chain_offset = cfg->chain_offset;
+  k.warmup = cfg->warmup;
+  k.samples = cfg->samples;
+  k.max_depth = cfg->max_treedepth;
+  k.save_warmup = cfg->save_warmup ? 1 : 0;
+  k.adapt = cfg->adapt_engaged ? 1 : 0;
+  k.seed = cfg->seed;
+  k.adapt_delta = cfg->adapt_delta;
+  k.gamma = cfg->gamma > 0 ? cfg->gamma : 0.05;
+  k.kappa = cfg->kappa > 0 ? cfg->kappa : 0.75;
+  k.t0 = cfg->t0 > 0 ? cfg->t0 : 10.0;
+  k.stepsize0 = cfg->stepsize;
+  k.init_radius = cfg->init_radius;
+  k.init_buffer = cfg->init_buffer;
+  k.term_buffer = cfg->term_buffer;
+  k.base_window = cfg->window;
+  const long long iters = (long long)cfg->warmup + cfg->samples;
+  k.max_steps = iters * ((1LL << cfg->max_treedepth) + 1) + 4000LL * (cfg->warmup / 10 + 4) + 10000;
+  k.iters_saved = cfg->save_warmup ? (int)iters : cfg->samples;
+  k.ncols = D + 8;
+  pl->draws_bytes = sizeof(double) * (size_t)C * k.iters_saved * k.ncols;
+  const int vlen = WAVE * pl->ppl;
+  auto setup = [&]() -> int {
+    HIP_TRY(hipMalloc(&pl->d_stack, sizeof(double) * (size_t)C * cfg->max_treedepth * NSTK * vlen));
+    HIP_TRY(hipMalloc(&pl->d_fin, sizeof(double) * (size_t)C * (1 + 2 * D)));
+    HIP_TRY(hipMalloc(&pl->d_status, sizeof(int) * C));
+    HIP_TRY(hipMalloc(&pl->d_leap, sizeof(long long) * C));
+    HIP_TRY(hipEventCreate(&pl->ev0));
+    HIP_TRY(hipEventCreate(&pl->ev1));
+    return FITOCT_OK;
+  };
+  rc = setup();
+  if (rc) {
+    free_plan(pl);
+    return rc;
+  }
+  k.stack = pl->d_stack;
+  k.fin_eps = pl->d_fin;
+  k.fin_minv = pl->d_fin + C;
+  k.fin_q = pl->d_fin + C + (size_t)C * D;
+  k.chain_status = pl->d_status;
+  k.leapfrogs = pl->d_leap;
+  *out = pl;
+  return FITOCT_OK;
+}
+
+int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
+  if (!pl || !info) return fail(FITOCT_E_ARG, "NULL argument");
+  info->dim = pl->kp.D;
+  info->n_cols = pl->kp.ncols;
+  info->iters_saved = pl->kp.iters_saved;
+  info->chains = pl->kp.chains;
+  info->tiles = pl->tiles;
+  info->chains_per_tile = pl->kp.G;
+  info->bins_per_thread = pl->bpt;
+  info->threads_per_tile = TPB;
+  info->lds_bytes = pl->lds;
+  info->n_pad = pl->kp.n_pad;
+  info->draws_bytes = (int64_t)pl->draws_bytes;
+  return FITOCT_OK;
+}
+
+int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
+  if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+  HIP_TRY(hipSetDevice(pl->cfg.device));
+  double* dst = (double*)d_draws;
+  if (!dst) {
+    if (!pl->d_draws) HIP_TRY(hipMalloc(&pl->d_draws, pl->draws_bytes));
+    dst = pl->d_draws;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  KParams k = pl->kp;
+  k.draws = dst;
+  HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * k.chains, st));
+  HIP_TRY(hipEventRecord(pl->ev0, st));
+  HIP_TRY(launch(false, pl->mixed, pl->bpt, pl->nnp, k, pl->tiles, st));
+  HIP_TRY(hipEventRecord(pl->ev1, st));
+  HIP_TRY(hipEventSynchronize(pl->ev1));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
+  pl->kernel_ms = ms;
+  pl->last_draws = dst;
+  pl->ran = true;
+  return FITOCT_OK;
+}
+
+int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
+  if (!pl || !res) return fail(FITOCT_E_ARG, "NULL argument");
+  if (!pl->ran) return fail(FITOCT_E_ARG, "plan has not run");
+  HIP_TRY(hipSetDevice(pl->cfg.device));
+  const KParams& k = pl->kp;
+  const int C = k.chains, D = k.D;
+  res->n_cols = k.ncols;
+  res->iters_saved = k.iters_saved;
+  res->dim = D;
+  res->kernel_ms = pl->kernel_ms;
+  if (res->draws) {
+    const int64_t need = (int64_t)C * k.iters_saved * k.ncols;
+    if (res->draws_capacity < need) return fail(FITOCT_E_ARG, "draws buffer too small");
+    HIP_TRY(hipMemcpy(res->draws, pl->last_draws, pl->draws_bytes, hipMemcpyDeviceToHost));
+  }
+  if (res->stepsize) HIP_TRY(hipMemcpy(res->stepsize, k.fin_eps, sizeof(double) * C, hipMemcpyDeviceToHost));
+  if (res->inv_metric)
+    HIP_TRY(hipMemcpy(res->inv_metric, k.fin_minv, sizeof(double) * C * D, hipMemcpyDeviceToHost));
+  if (res->last_q) HIP_TRY(hipMemcpy(res->last_q, k.fin_q, sizeof(double) * C * D, hipMemcpyDeviceToHost));
+  std::vector<int> st(C);
+  HIP_TRY(hipMemcpy(st.data(), k.chain_status, sizeof(int) * C, hipMemcpyDeviceToHost));
+  if (res->chain_status) memcpy(res->chain_status, st.data(), sizeof(int) * C);
+  std::vector<long long> lf(C);
+  HIP_TRY(hipMemcpy(lf.data(), k.leapfrogs, sizeof(long long) * C, hipMemcpyDeviceToHost));
+  long long tot = 0;
+  for (long long v : lf) tot += v;
+  res->total_leapfrogs = tot;
+  for (int c = 0; c < C; ++c)
+    if (st[c] != 0) {
+      return fail(st[c], "chain " + std::to_string(k.chain_offset + c) + " failed with status " +
+                             std::to_string(st[c]));
+    }
+  return FITOCT_OK;
+}
+
+void fitoct_plan_destroy(fitoct_plan* pl) { free_plan(pl); }
+
+int32_t fitoct_expgp_sample(const fitoct_problem* prob, const fitoct_config* cfg,
+                            fitoct_result* res) {
+  const auto t0 = std::chrono::steady_clock::now();
+  fitoct_plan* pl = nullptr;
+  int rc = fitoct_plan_create(prob, cfg, &pl);
+  if (rc) return rc;
+  rc = fitoct_plan_run(pl, nullptr, nullptr);
+  if (!rc && res) rc = fitoct_plan_download(pl, res);
+  free_plan(pl);
+  if (res)
+    res->wall_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
+int32_t fitoct_split_rhat_ess(const double* x, int32_t chains, int32_t n, double* rhat,
+                              double* ess) {
+  if (!x) return fail(FITOCT_E_ARG, "x is NULL");
+  return split_rhat_ess(x, chains, n, rhat, ess);
+}
+
+int32_t fitoct_rank_rhat(const double* x, int32_t chains, int32_t n, double* rhat) {
+  if (!x || !rhat) return fail(FITOCT_E_ARG, "NULL argument");
+  return rank_rhat(x, chains, n, rhat);
+}
+
+}  // extern "C"

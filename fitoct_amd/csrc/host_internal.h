@@ -1,0 +1,19 @@
+// Internal declarations shared by the host translation units of libfitoct.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "fitoct.h"
+
+namespace fitoct {
+
+extern thread_local std::string g_last_error;
+int fail(int code, const std::string& msg);
+
+int build_basis(const fitoct_problem* p, std::vector<double>& B, std::vector<double>& xg);
+int model_dim(int prior, int Nn);
+std::string column_name(int prior, int Nn, int i);
+int split_rhat_ess(const double* x, int chains, int n, double* rhat, double* ess);
+int rank_rhat(const double* x, int chains, int n, double* out);
+
+}  // namespace fitoct

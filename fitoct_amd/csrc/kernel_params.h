@@ -1,0 +1,67 @@
+// Launch parameters shared by the host planner (fitoct_api.cpp) and the device
+// sampler (nuts_device.hip).  Plain data, passed by value as a kernel argument.
+#pragma once
+#include <stdint.h>
+
+namespace fitoct {
+
+constexpr int WAVE = 64;          // CDNA wavefront
+constexpr int NW = 16;            // waves per tile (workgroup)
+constexpr int TPB = NW * WAVE;    // 1024 threads per tile (4 waves per SIMD)
+constexpr int GMAX = 8;           // max chains per tile (one NUTS wave each)
+constexpr int MAXDEPTH = 16;      // hard cap on max_treedepth
+constexpr int NSLOT = 32;         // reduced sums per chain (4 + NNP <= 32)
+constexpr int MPW = 32;           // model-parameter words per chain (theta[3], pad, yGP[NNP])
+constexpr int NSTK = 6;           // vectors per tree level in the global stack
+constexpr int KMAX = 24;          // max GP control points (K^-1 tile in LDS)
+
+// how a tile evaluates the GP modulation dL = B yGP and its adjoint B^T h
+enum BasisMode : int {
+  MODE_POLY = 0,    // factorised SE basis: per-bin (t, a) in VGPRs, Horner + moments (f64)
+  MODE_BREG = 1,    // basis rows resident in VGPRs (user basis / fp32)
+  MODE_STREAM = 2,  // basis rows streamed from global memory each pass (large N)
+};
+
+enum ChainState : int { ST_INIT = 0, ST_STEPSIZE = 1, ST_TREE = 2, ST_DONE = 3 };
+
+struct KParams {
+  // ---- data (device pointers, padded to n_pad bins) ----
+  const void* cx;      // R[n_pad]  c * x_i
+  const void* y;       // R[n_pad]
+  const void* isu;     // R[n_pad]  1/uy_i (0 on padding)
+  const void* B;       // BREG/STREAM: R[n_pad][NNP] basis rows; POLY: R[n_pad][2] (t, a)
+  const double* Kinv;  // POLY: [Nn][Nn] (K(xGP,xGP) + nugget I)^-1
+  const double* bvec;  // POLY: [Nn] b_l
+  int N, n_pad, Nn, D, family, prior_PD, mode;
+  double theta0[3];
+  double S0inv[9];
+  double lambda_rate_eff;   // rate of the exponential prior on lambda (normal family)
+  double lambda_scale;      // lasso lambda_s
+  double nu;                // horseshoe nu
+  double sigma_scale;
+  // ---- sampler ----
+  int chains;               // chains in this launch
+  int chain_offset;         // global id of chain 0
+  int G;                    // chains per tile
+  int warmup, samples, max_depth, save_warmup, adapt;
+  uint64_t seed;
+  double adapt_delta, gamma, kappa, t0, stepsize0, init_radius;
+  int init_buffer, term_buffer, base_window;
+  long long max_steps;      // per-tile step bound (termination guarantee)
+  // ---- outputs ----
+  double* draws;            // [chains][iters_saved][ncols]
+  int ncols, iters_saved;
+  double* stack;            // [chains][max_depth][NSTK][vlen]
+  double* fin_eps;          // [chains]
+  double* fin_minv;         // [chains][D]
+  double* fin_q;            // [chains][D]
+  int* chain_status;        // [chains]
+  long long* leapfrogs;     // [chains]
+  // ---- logp mode ----
+  const double* q_in;       // [points][D]
+  double* lp_out;           // [points]
+  double* grad_out;         // [points][D]
+  double* s2_out;           // [points]
+};
+
+}  // namespace fitoct

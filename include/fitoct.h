@@ -1,0 +1,187 @@
+/*
+ * fitoct.h -- C ABI of libfitoct.so, the MI355X-native NUTS sampler for FitOCT's
+ * modulated-exponential (ExpGP) posterior.
+ *
+ * This is the drop-in boundary of SURVEY.md §8b.  In the reference, the hot path
+ * is reached from R through FitOCTLib::fitExpGP (external package; called at
+ * FitOCT.R:110-124, priPost.R:2-16, ShinyInterface/server.R:408-426), which hands
+ * a Stan data list to rstan::sampling (chains fanned out over R worker processes,
+ * FitOCT.R:13).  libfitoct replaces rstan::sampling + the Stan C++ model/NUTS with:
+ *
+ *   fitoct_expgp_sample()   <- FitOCTLib::fitExpGP(method='sample') -> rstan::sampling
+ *                              (FitOCT.R:110-124 / priPost.R:2-16 / server.R:408-426)
+ *   fitoct_logp_grad()      <- Stan model log_prob + stan-math gradient
+ *                              (the ExpGP model whose parameters are named at plotExpGP.R:9,41)
+ *   fitoct_build_basis()    <- the GP design of server.R:623-650 (xGP grid, SE kernel)
+ *   fitoct_split_rhat_ess() <- rstan::summary(...)$summary[, c('n_eff','Rhat')]
+ *                              (server.R:88-104,189-213)
+ *   fitoct_plan_*()         <- same as fitoct_expgp_sample, split so that inputs can stay
+ *                              resident in HBM across calls and draws can land in a
+ *                              caller-owned device buffer (multi-GPU gather / benchmarking)
+ *
+ * Conventions: plain C types only; every host buffer is owned by the caller; the
+ * library never keeps a caller pointer after returning; device memory it allocates
+ * is released on return or by fitoct_plan_destroy().  Functions return
+ * FITOCT_OK (0) or a negative fitoct_status; fitoct_last_error() then describes
+ * the failure (thread-local string).  No C++ exception crosses this boundary.
+ */
+#ifndef FITOCT_H
+#define FITOCT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FITOCT_ABI_VERSION 1
+
+typedef enum fitoct_status {
+  FITOCT_OK = 0,
+  FITOCT_E_ARG = -1,       /* invalid argument / unsupported shape */
+  FITOCT_E_HIP = -2,       /* HIP runtime error */
+  FITOCT_E_NODEVICE = -3,  /* no HIP device visible */
+  FITOCT_E_INIT = -4,      /* no finite initial point after 100 attempts */
+  FITOCT_E_NUMERIC = -5,   /* step size search diverged (eps > 1e7 or eps == 0) */
+  FITOCT_E_TIMEOUT = -6,   /* device step bound reached before all chains finished */
+  FITOCT_E_INTERNAL = -7
+} fitoct_status;
+
+/* yGP hyper-prior families */
+enum { FITOCT_PRIOR_NORMAL = 0, FITOCT_PRIOR_LASSO = 1, FITOCT_PRIOR_HORSESHOE = 2 };
+/* GP control grid (server.R:627-631) */
+enum { FITOCT_GRID_INTERNAL = 0, FITOCT_GRID_EXTREMAL = 1 };
+/* arithmetic of the per-bin likelihood sweep; reductions and sampler state are f64 always */
+enum { FITOCT_PREC_F64 = 0, FITOCT_PREC_MIXED = 1 };
+
+/* Inputs of FitOCTLib::fitExpGP (same meaning, FitOCT.R:110-124) plus the ⚑ model switches. */
+typedef struct fitoct_problem {
+  int32_t N;             /* depth bins */
+  const double* x;       /* [N] depth (um), strictly increasing not required, max > min */
+  const double* y;       /* [N] intensity / amplitude */
+  const double* uy;      /* [N] data uncertainty (> 0) */
+  int32_t data_type;     /* c in exp(-c*x/theta3): 1 amplitude, 2 intensity (FitOCT.R:39) */
+  int32_t Nn;            /* GP control points, 2..24 (ui.R:200-207 allows 5..20) */
+  int32_t grid_type;     /* FITOCT_GRID_* */
+  double rho;            /* GP length scale on normalised depth; <= 0 -> 1/Nn (FitOCT.R:119) */
+  const double* B;       /* optional [N*Nn] row-major basis; NULL -> fitoct_build_basis */
+  double theta0[3];      /* prior mean of theta (estimateExpPrior, FitOCT.R:103-107) */
+  double Sigma0[9];      /* prior covariance of theta, row-major */
+  int32_t prior_type;    /* FITOCT_PRIOR_* */
+  double lambda_rate;    /* normal family: lambda ~ Exponential (see lambda_conv) (FitOCT.R:47) */
+  double lambda_scale;   /* lasso family: lambda_s of lassoPrior.stan:4 */
+  double nu;             /* horseshoe family: nu of horseShoePrior.stan:13 (1 = horseshoe) */
+  int32_t prior_PD;      /* 1: likelihood off (prior predictive, priPost.R:14) */
+  int32_t kernel_conv;   /* ⚑ 0: exp(-d^2/(2 rho^2)) (Stan), 1: exp(-(d/rho)^2) (RMgauss) */
+  int32_t lambda_conv;   /* ⚑ 0: rate = 1/lambda_rate, 1: rate = lambda_rate */
+  double sigma_scale;    /* ⚑ sigma ~ half-normal(0, sigma_scale) */
+  double nugget;         /* diagonal jitter of K(xGP,xGP) (1e-9) */
+} fitoct_problem;
+
+/* rstan::sampling controls (testGamma.R:42-47) + sharding / device selection. */
+typedef struct fitoct_config {
+  int32_t chains;        /* chains run by THIS call */
+  int32_t chain_offset;  /* global id of the first chain: RNG stream = (seed, chain id) */
+  int32_t warmup;        /* nb_warmup */
+  int32_t samples;       /* nb_iter - nb_warmup */
+  uint64_t seed;
+  double adapt_delta;    /* 0.8 */
+  int32_t max_treedepth; /* 10 (1..16) */
+  int32_t adapt_engaged; /* 1 */
+  double stepsize;       /* initial step size (1) */
+  double gamma, kappa, t0;                     /* dual averaging: 0.05, 0.75, 10 */
+  int32_t init_buffer, term_buffer, window;    /* 75, 50, 25 */
+  double init_radius;    /* jitter around the default init (0 -> deterministic) */
+  int32_t save_warmup;   /* 1: warmup draws are stored too (traceplot(inc_warmup=TRUE)) */
+  int32_t precision;     /* FITOCT_PREC_* */
+  int32_t device;        /* HIP device ordinal */
+} fitoct_config;
+
+/* Outputs; every pointer is caller-allocated (NULL = not wanted). */
+typedef struct fitoct_result {
+  double* draws;            /* [chains][iters_saved][n_cols], see fitoct_column_name */
+  int64_t draws_capacity;   /* elements available at draws */
+  double* stepsize;         /* [chains] adapted step size */
+  double* inv_metric;       /* [chains][D] adapted diagonal inverse metric */
+  double* last_q;           /* [chains][D] final unconstrained position */
+  int32_t* chain_status;    /* [chains] 0 or a fitoct_status per chain */
+  int32_t n_cols;           /* out */
+  int32_t iters_saved;      /* out */
+  int32_t dim;              /* out: D, unconstrained dimension */
+  int32_t pad_;
+  int64_t total_leapfrogs;  /* out: sum of n_leapfrog__ over every transition of every chain */
+  double kernel_ms;         /* out: device time of the sampler kernel (HIP events) */
+  double wall_ms;           /* out: host wall time of the call */
+} fitoct_result;
+
+/* Static description of a planned run. */
+typedef struct fitoct_plan_info {
+  int32_t dim;             /* D */
+  int32_t n_cols;          /* D + 8 */
+  int32_t iters_saved;
+  int32_t chains;
+  int32_t tiles;           /* workgroups launched */
+  int32_t chains_per_tile; /* G */
+  int32_t bins_per_thread; /* 0 = streamed from global memory */
+  int32_t threads_per_tile;
+  int32_t lds_bytes;
+  int32_t n_pad;           /* padded bin count */
+  int64_t draws_bytes;     /* size of the draws buffer */
+} fitoct_plan_info;
+
+typedef struct fitoct_plan fitoct_plan;
+
+/* ---- library ---------------------------------------------------------- */
+int32_t fitoct_abi_version(void);
+const char* fitoct_last_error(void);
+int32_t fitoct_device_count(void);
+/* sizeof of the ABI structs, so bindings can assert their layout */
+int32_t fitoct_struct_sizes(int32_t* problem, int32_t* config, int32_t* result, int32_t* info);
+void fitoct_default_config(fitoct_config* cfg);
+void fitoct_default_problem(fitoct_problem* prob);
+
+/* ---- model layout (host only) -------------------------------------------- */
+int32_t fitoct_dim(int32_t prior_type, int32_t Nn);
+int32_t fitoct_n_cols(int32_t prior_type, int32_t Nn);
+/* Stan-CSV style name of draw column i (lp__, accept_stat__, ..., theta.1, ...) */
+int32_t fitoct_column_name(int32_t prior_type, int32_t Nn, int32_t i, char* buf, int32_t buflen);
+
+/* ---- GP basis (host only, fp64 Cholesky) --------------------------------- */
+int32_t fitoct_build_basis(const fitoct_problem* prob, double* B_out /*[N*Nn]*/,
+                           double* xGP_out /*[Nn] or NULL*/);
+
+/* ---- hot path ------------------------------------------------------------ */
+/* log density and gradient at n_points unconstrained positions q[n_points][D]
+ * (host buffers); lp_out[n_points], grad_out[n_points][D], sumr2_out[n_points]
+ * (sum(((y-m)/uy)^2), NULL allowed). */
+int32_t fitoct_logp_grad(const fitoct_problem* prob, int32_t n_points, const double* q,
+                         double* lp_out, double* grad_out, double* sumr2_out,
+                         int32_t precision, int32_t device);
+
+/* one-shot: plan + run + download + destroy */
+int32_t fitoct_expgp_sample(const fitoct_problem* prob, const fitoct_config* cfg,
+                            fitoct_result* res);
+
+int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
+                           fitoct_plan** out);
+int32_t fitoct_plan_get_info(const fitoct_plan* plan, fitoct_plan_info* info);
+/* Run the sampler on `stream` (hipStream_t; NULL = default stream).  If d_draws is
+ * non-NULL the draws go to that caller-owned DEVICE buffer (>= info.draws_bytes),
+ * otherwise to a plan-internal one.  Returns after the kernel completes. */
+int32_t fitoct_plan_run(fitoct_plan* plan, void* d_draws, void* stream);
+/* Copy the last run's outputs to host buffers of `res`. */
+int32_t fitoct_plan_download(fitoct_plan* plan, fitoct_result* res);
+void fitoct_plan_destroy(fitoct_plan* plan);
+
+/* ---- diagnostics (host only) ---------------------------------------------- */
+/* x[chains][n] of one scalar: rstan legacy split-R-hat and n_eff (autocorrelation,
+ * Geyer initial monotone sequence), as shown by rstan::summary (server.R:88-104). */
+int32_t fitoct_split_rhat_ess(const double* x, int32_t chains, int32_t n,
+                              double* rhat, double* ess);
+/* rank-normalised split-R-hat (Vehtari et al. 2021), max of bulk and folded. */
+int32_t fitoct_rank_rhat(const double* x, int32_t chains, int32_t n, double* rhat);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FITOCT_H */
