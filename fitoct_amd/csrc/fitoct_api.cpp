@@ -4,6 +4,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -16,9 +17,9 @@
 #include "kernel_params.h"
 
 namespace fitoct {
-hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P, int tiles,
-                  hipStream_t st);
-int lds_bytes(int ppl, int G);
+hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P, const KParams* dP,
+                  int tiles, hipStream_t st);
+int lds_bytes(int ppl, int G, int max_depth);
 }  // namespace fitoct
 
 using namespace fitoct;
@@ -43,6 +44,7 @@ struct fitoct_plan {
   double* d_fin = nullptr;    // eps[C] | minv[C*D] | q[C*D]
   int* d_status = nullptr;
   long long* d_leap = nullptr;
+  KParams* d_kp = nullptr;    // device copy of the launch parameters
   double* last_draws = nullptr;
   double kernel_ms = 0.0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -93,14 +95,14 @@ int invert3(const double* S, double* Si) {
   return FITOCT_OK;
 }
 
-// Shapes: bins are strided over the 1024 lanes of a tile; up to 4 bins per lane
-// keep their data in registers (MODE_POLY: 5 values per bin; MODE_BREG: 3 + NNP
-// fp32 values, up to 2 bins), beyond that the basis rows are streamed.
+// Shapes: bins are strided over the 512 lanes of a tile's gradient waves; up to
+// 4 bins per lane keep their data in VGPRs for the whole run (MODE_POLY: 5 f64
+// values per bin; MODE_ROWS: 3 + NNP fp32 values), beyond that they are streamed.
 void choose_bins(int N, int& bpt, int& n_pad) {
-  if (N <= TPB) { bpt = 1; n_pad = TPB; }
-  else if (N <= 2 * TPB) { bpt = 2; n_pad = 2 * TPB; }
-  else if (N <= 4 * TPB) { bpt = 4; n_pad = 4 * TPB; }
-  else { bpt = 0; n_pad = (N + TPB - 1) / TPB * TPB; }
+  if (N <= GT) { bpt = 1; n_pad = GT; }
+  else if (N <= 2 * GT) { bpt = 2; n_pad = 2 * GT; }
+  else if (N <= 4 * GT) { bpt = 4; n_pad = 4 * GT; }
+  else { bpt = 0; n_pad = (N + GT - 1) / GT * GT; }
 }
 
 // MODE_POLY factors of the SE basis on the uniform grid g_l = g_0 + l*dg:
@@ -213,7 +215,8 @@ void stage(const fitoct_problem* p, const std::vector<double>& B, const std::vec
 }
 
 // common planning for the sampler and the logp kernel
-int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precision, int device) {
+int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precision, int device,
+                int max_depth) {
   int rc = check_problem(p);
   if (rc) return rc;
   int ndev = 0;
@@ -246,13 +249,13 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   std::vector<double> ta, kinv, bv;
   int mode;
   if (pl->mixed) {
-    mode = (pl->bpt == 1 || pl->bpt == 2) ? MODE_BREG : MODE_STREAM;
+    mode = MODE_ROWS;
   } else {
-    const bool poly = !p->B && pl->bpt > 0 && getenv("FITOCT_NO_POLY") == nullptr &&
+    const bool poly = !p->B && getenv("FITOCT_NO_POLY") == nullptr &&
                       build_poly(p, B, pl->nnp, ta, kinv, bv);
-    mode = poly ? MODE_POLY : MODE_STREAM;
+    mode = poly ? MODE_POLY : MODE_ROWS;
+    if (mode == MODE_ROWS) pl->bpt = 0;   // f64 rows are streamed (16 doubles per bin)
   }
-  if (mode == MODE_STREAM) pl->bpt = 0;
   std::vector<char> staged;
   if (pl->mixed) stage<float>(p, B, ta, mode, n_pad, pl->nnp, staged);
   else stage<double>(p, B, ta, mode, n_pad, pl->nnp, staged);
@@ -292,10 +295,13 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   // chains per tile: fill every CU with one tile first, then stack chains
   const int ncu = std::max(1, prop.multiProcessorCount);
   int G = std::max(1, std::min(GMAX, (chains + ncu - 1) / ncu));
-  while (G > 1 && lds_bytes(pl->ppl, G) > 160 * 1024 - 256) --G;
+  while (G > 1 && lds_bytes(pl->ppl, G, max_depth) > 160 * 1024 - 256) --G;
+  if (lds_bytes(pl->ppl, G, max_depth) > 160 * 1024 - 256)
+    return fail(FITOCT_E_ARG, "max_treedepth too large for the LDS budget");
   k.G = G;
+  k.max_depth = max_depth;
   pl->tiles = (chains + G - 1) / G;
-  pl->lds = lds_bytes(pl->ppl, G);
+  pl->lds = lds_bytes(pl->ppl, G, max_depth);
   return FITOCT_OK;
 }
 
@@ -307,6 +313,7 @@ void free_plan(fitoct_plan* pl) {
   (void)hipFree(pl->d_fin);
   (void)hipFree(pl->d_status);
   (void)hipFree(pl->d_leap);
+  (void)hipFree(pl->d_kp);
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
   if (pl->ev1) (void)hipEventDestroy(pl->ev1);
   delete pl;
@@ -405,7 +412,7 @@ int32_t fitoct_logp_grad(const fitoct_problem* prob, int32_t n_points, const dou
                          int32_t device) {
   if (n_points < 1 || !q || !lp_out || !grad_out) return fail(FITOCT_E_ARG, "bad buffers");
   fitoct_plan* pl = new fitoct_plan();
-  int rc = plan_common(pl, prob, n_points, precision, device);
+  int rc = plan_common(pl, prob, n_points, precision, device, 0);
   if (rc) {
     free_plan(pl);
     return rc;
@@ -421,7 +428,9 @@ int32_t fitoct_logp_grad(const fitoct_problem* prob, int32_t n_points, const dou
     k.grad_out = d_out;
     k.lp_out = d_out + (size_t)n_points * D;
     k.s2_out = k.lp_out + n_points;
-    HIP_TRY(launch(true, pl->mixed, pl->bpt, pl->nnp, k, pl->tiles, 0));
+    HIP_TRY(hipMalloc(&pl->d_kp, sizeof(KParams)));
+    HIP_TRY(hipMemcpy(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
+    HIP_TRY(launch(true, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, 0));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(grad_out, d_out, sizeof(double) * (size_t)n_points * D, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(lp_out, k.lp_out, sizeof(double) * n_points, hipMemcpyDeviceToHost));
@@ -449,7 +458,7 @@ int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
     return fail(FITOCT_E_ARG, "adapt_delta must be in (0, 1)");
   if (!(cfg->stepsize > 0.0)) return fail(FITOCT_E_ARG, "stepsize must be > 0");
   fitoct_plan* pl = new fitoct_plan();
-  int rc = plan_common(pl, prob, cfg->chains, cfg->precision, cfg->device);
+  int rc = plan_common(pl, prob, cfg->chains, cfg->precision, cfg->device, cfg->max_treedepth);
   if (rc) {
     free_plan(pl);
     return rc;
@@ -480,7 +489,7 @@ int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
   pl->draws_bytes = sizeof(double) * (size_t)C * k.iters_saved * k.ncols;
   const int vlen = WAVE * pl->ppl;
   auto setup = [&]() -> int {
-    HIP_TRY(hipMalloc(&pl->d_stack, sizeof(double) * (size_t)C * cfg->max_treedepth * NSTK * vlen));
+    HIP_TRY(hipMalloc(&pl->d_stack, sizeof(double) * (size_t)C * (cfg->max_treedepth + 1) * 3 * vlen));
     HIP_TRY(hipMalloc(&pl->d_fin, sizeof(double) * (size_t)C * (1 + 2 * D)));
     HIP_TRY(hipMalloc(&pl->d_status, sizeof(int) * C));
     HIP_TRY(hipMalloc(&pl->d_leap, sizeof(long long) * C));
@@ -531,14 +540,49 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
   KParams k = pl->kp;
   k.draws = dst;
   HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * k.chains, st));
+  long long* d_stamps = nullptr;
+  const bool want_stamps = getenv("FITOCT_STAMPS") != nullptr;   // diagnostic only
+  if (want_stamps) {
+    HIP_TRY(hipMalloc(&d_stamps, sizeof(long long) * 40 * pl->tiles));
+    HIP_TRY(hipMemsetAsync(d_stamps, 0, sizeof(long long) * 40 * pl->tiles, st));
+    k.stamps = d_stamps;
+  }
   HIP_TRY(hipEventRecord(pl->ev0, st));
-  HIP_TRY(launch(false, pl->mixed, pl->bpt, pl->nnp, k, pl->tiles, st));
+  if (!pl->d_kp) HIP_TRY(hipMalloc(&pl->d_kp, sizeof(KParams)));
+  HIP_TRY(hipMemcpyAsync(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice, st));
+  HIP_TRY(launch(false, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, st));
   HIP_TRY(hipEventRecord(pl->ev1, st));
   HIP_TRY(hipEventSynchronize(pl->ev1));
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
   pl->kernel_ms = ms;
   pl->last_draws = dst;
+  if (want_stamps) {
+    std::vector<long long> h((size_t)40 * pl->tiles);
+    HIP_TRY(hipMemcpy(h.data(), d_stamps, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
+    (void)hipFree(d_stamps);
+    double steps = 0, tg = 0, tn = 0, tt = 0, smax = 0;
+    double act_t[18] = {0}, act_n[18] = {0};
+    for (int t = 0; t < pl->tiles; ++t) {
+      steps += h[40 * t];
+      tg += h[40 * t + 1];
+      tn += h[40 * t + 2];
+      tt += h[40 * t + 3];
+      smax = std::max(smax, (double)h[40 * t]);
+      for (int a = 0; a < 18; ++a) {
+        act_t[a] += h[40 * t + 4 + a];
+        act_n[a] += h[40 * t + 22 + a];
+      }
+    }
+    fprintf(stderr, "[fitoct stamps] per action (chain 0 of each tile): ");
+    for (int a = 1; a < 18; ++a)
+      if (act_n[a] > 0) fprintf(stderr, "a%d:%.0fx%.0f ", a, act_n[a] / pl->tiles, act_t[a] / act_n[a]);
+    fprintf(stderr, "\n");
+    fprintf(stderr,
+            "[fitoct stamps] tiles=%d mean sweeps/tile=%.0f max=%.0f | per sweep: grad-wave busy %.0f "
+            "nuts-wave busy %.0f wall %.0f memtime ticks\n",
+            pl->tiles, steps / pl->tiles, smax, tg / steps, tn / steps, tt / steps);
+  }
   pl->ran = true;
   return FITOCT_OK;
 }

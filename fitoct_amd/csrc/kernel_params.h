@@ -6,20 +6,23 @@
 namespace fitoct {
 
 constexpr int WAVE = 64;          // CDNA wavefront
-constexpr int NW = 16;            // waves per tile (workgroup)
-constexpr int TPB = NW * WAVE;    // 1024 threads per tile (4 waves per SIMD)
-constexpr int GMAX = 8;           // max chains per tile (one NUTS wave each)
+constexpr int NW = 12;            // waves per tile (workgroup): 3 per SIMD -> 168 VGPRs each
+constexpr int TPB = NW * WAVE;    // 768 threads per tile
+constexpr int NGW = 8;            // gradient waves (waves 0..7): the likelihood sweep
+constexpr int GT = NGW * WAVE;    // 512 gradient lanes; bins are strided over them
+constexpr int GMAX = NW - NGW;    // NUTS waves (8..11), one chain each: max chains per tile
 constexpr int MAXDEPTH = 16;      // hard cap on max_treedepth
 constexpr int NSLOT = 32;         // reduced sums per chain (4 + NNP <= 32)
 constexpr int MPW = 32;           // model-parameter words per chain (theta[3], pad, yGP[NNP])
 constexpr int NSTK = 6;           // vectors per tree level in the global stack
 constexpr int KMAX = 24;          // max GP control points (K^-1 tile in LDS)
 
-// how a tile evaluates the GP modulation dL = B yGP and its adjoint B^T h
+// how a tile evaluates the GP modulation dL = B yGP and its adjoint B^T h.
+// With BPT > 0 a lane's bins stay in VGPRs for the whole run, with BPT == 0 the
+// bins are streamed from global memory (L2-resident) on every pass.
 enum BasisMode : int {
-  MODE_POLY = 0,    // factorised SE basis: per-bin (t, a) in VGPRs, Horner + moments (f64)
-  MODE_BREG = 1,    // basis rows resident in VGPRs (user basis / fp32)
-  MODE_STREAM = 2,  // basis rows streamed from global memory each pass (large N)
+  MODE_POLY = 0,    // factorised SE basis: per-bin (t, a), Horner + moments (f64 path)
+  MODE_ROWS = 1,    // explicit basis rows B[i, 0..NNP) (user basis, fp32 path)
 };
 
 enum ChainState : int { ST_INIT = 0, ST_STEPSIZE = 1, ST_TREE = 2, ST_DONE = 3 };
@@ -57,6 +60,7 @@ struct KParams {
   double* fin_q;            // [chains][D]
   int* chain_status;        // [chains]
   long long* leapfrogs;     // [chains]
+  long long* stamps;        // optional [tiles][4]: half-steps, gradient busy, NUTS busy, total cycles
   // ---- logp mode ----
   const double* q_in;       // [points][D]
   double* lp_out;           // [points]

@@ -3,29 +3,42 @@
 // Replaces rstan::sampling + Stan's base_nuts / adapt_diag_e_nuts + the
 // stanc-generated model with stan-math AD.
 //
-// Execution model ("tile" = one 512-thread workgroup, persistent for the whole run):
-//   * a tile owns G <= 8 chains that advance in LOCK-STEP, one leapfrog per
-//     chain per tile step.  Each chain is an explicit state machine (init ->
-//     step-size search -> tree building -> adaptation -> next transition), so a
-//     chain that finishes its trajectory simply starts its next transition on
-//     the next step: no chain ever waits for another chain's tree.
-//   * gradient phase (all 16 waves): the N depth bins are strided over the
-//     1024 lanes; each lane keeps its bins' data resident in VGPRs for the
+// Execution model ("tile" = one 768-thread workgroup, persistent for the whole run):
+//   * a tile owns G <= 4 chains.  Each chain is an explicit state machine (init
+//     -> step-size search -> tree building -> adaptation -> next transition)
+//     that consumes one gradient per leapfrog, so a chain that finishes its
+//     trajectory starts its next transition at once: no chain waits for
+//     another chain's tree.
+//   * the 12 waves are specialised: waves 0..7 only run the likelihood sweep,
+//     waves 8..11 only run NUTS (one chain each), so neither role's registers
+//     are live in the other's code.  The roles meet in a dataflow pipeline
+//     through LDS: a NUTS wave enqueues its chain's next position in a ring,
+//     the gradient waves drain the ring in order and count their completions
+//     per chain, the NUTS wave resumes when all 8 sweeps are in.  No barrier
+//     after start-up: each chain's sampler latency hides behind the sweeps of
+//     the tile's other chains.
+//   * gradient waves: the N depth bins are strided over 512 lanes; each lane
+//     keeps its bins' data resident in VGPRs for the
 //     whole run (read from HBM once per tile, shared by all G chains).  For the
 //     built-in uniform-grid SE basis (MODE_POLY) the GP basis factorises as
 //     K(x~_i, g_l) = a_i t_i^l b_l, so a bin needs 5 registers (c*x, y, 1/uy,
 //     t, a) instead of a 16-wide basis row: dL_i = a_i P(t_i) by Horner on the
 //     chain's coefficients c = b .* K^-1 yGP, and B^T h = K^-1 (b .* M) from
 //     the moments M_l = sum_i h_i a_i t_i^l.  A user-supplied basis keeps its
-//     rows in registers (MODE_BREG, fp32) or streams them (MODE_STREAM).
-//     Per chain a lane accumulates 4+NNP partial sums, a 64-lane transposed
-//     butterfly reduces them, and 16 per-wave partials land in LDS.
+//     rows in registers (MODE_ROWS, fp32) or streams them (MODE_STREAM).
+//     Per chain a lane accumulates 4+NNP partial sums; a transposed butterfly
+//     built from v_permlane32_swap / v_permlane16_swap / DPP row mirrors
+//     reduces them across the wave (no LDS round trips), and 8 per-wave
+//     partials land in LDS.
 //   * NUTS phase (wave c drives chain c): lane k holds parameter k.  The wave
-//     sums the 16 partials, completes lp / grad with the priors and the
-//     log-Jacobians, and advances the chain's state machine; Stan's recursive
-//     build_tree is replayed iteratively, one leaf per step, with a per-level
-//     stack (p_beg, p_end, rho, proposal q/p/g) kept in HBM (L2-resident).
-//   * two workgroup barriers per step; no inter-workgroup communication at all.
+//     sums the 8 partials, completes lp / grad with the priors and the
+//     log-Jacobians, and advances the chain's state machine.  Stan's recursive
+//     build_tree is replayed iteratively, one leaf per step: the U-turn records
+//     (p_beg, p_end, rho) of each tree level live in LDS, the multinomial
+//     proposals (q, p, grad) in a per-chain HBM pool addressed by slot index, so
+//     a proposal is written once when its leaf is pushed and read only when it
+//     becomes the sample.  Wave reductions are DPP/permlane butterflies.
+//   * no inter-workgroup communication at all.
 //
 // Random numbers are addressable Philox draws (philox.h), identical to the CPU
 // oracle's, so short horizons of GPU and CPU chains coincide draw for draw.
@@ -40,7 +53,7 @@
 namespace fitoct {
 
 enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2 };
-enum { ERR_INIT = -4, ERR_NUMERIC = -5 };
+enum { ERR_INIT = -4, ERR_NUMERIC = -5, ERR_TIMEOUT = -6 };
 
 // vectors kept in LDS per chain (lane-private elements)
 enum VecId : int {
@@ -50,21 +63,28 @@ enum VecId : int {
   V_SMP_Q, V_SMP_P, V_SMP_G,   // z_sample
   V_MINV, V_WF_M, V_WF_M2,     // metric + Welford
   V_RHO, V_PNEAR,              // trajectory momentum sum, near end of old trajectory
+  V_QS, V_QE,                  // staged q and its constrained values (exp on positive params)
   NVEC
 };
-// global stack vectors per tree level
-enum StkId : int { K_PBEG = 0, K_PEND = 1, K_RHO = 2, K_PQ = 3, K_PP = 4, K_PG = 5 };
+// U-turn record of one tree level (LDS)
+enum LvlId : int { K_PBEG = 0, K_PEND = 1, K_RHO = 2, NLVL = 3 };
+// proposal pool slot (HBM)
+enum PoolId : int { P_Q = 0, P_P = 1, P_G = 2, NPOOL = 3 };
+constexpr int NAUX = 64;   // per chain: yGP[32] | horseshoe lambda_j*tau [32]
 
 struct ChainScalars {
   int state, t, depth, leaf, dir, n_leapfrog, divergent, init_attempt;
   int da_counter, win_counter, win_size, win_next, wf_n, ss_trial, ss_dir, ss_window;
-  int status, win_on, init_buf, term_buf;
-  int pad0, pad1, pad2, pad3;
-  double H0, lsw, sum_metro, eps, eps_used, mu, s_bar, x_bar, ss_H0;
+  int status, win_on, init_buf, term_buf, pool_used, pad0, pad1, pad2;
+  int st_prop[MAXDEPTH];
+  double H0, lsw, sum_metro, eps, eps_used, mu, s_bar, x_bar, ss_H0, lf_e;
   double cur_lp, cur_s2, smp_lp, smp_s2;
   double end_lp[2], end_s2[2];
-  double st_lsw[MAXDEPTH], st_lp[MAXDEPTH], st_s2[MAXDEPTH];
+  double st_lsw[MAXDEPTH];
+  double pool_lp[MAXDEPTH + 1], pool_s2[MAXDEPTH + 1];
   long long leapfrogs;
+  long long pad3;
+  long long prof[2][32];   // diagnostic build: cycles and calls per action
 };
 static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
 
@@ -74,19 +94,64 @@ __device__ __forceinline__ void wave_fence() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-__device__ __forceinline__ double wave_sum(double x) {
-  // butterfly: every lane ends with the bitwise-identical sum (a+b == b+a)
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
-  return x;
+// ---------------------------------------------------------------------------
+// cross-lane moves of doubles without LDS (DPP row ops, gfx950 permlane swaps)
+// ---------------------------------------------------------------------------
+constexpr int DPP_XOR1 = 0xB1;         // quad_perm(1,0,3,2)
+constexpr int DPP_XOR2 = 0x4E;         // quad_perm(2,3,0,1)
+constexpr int DPP_QREV = 0x1B;         // quad_perm(3,2,1,0): flip bits 0,1
+constexpr int DPP_HALF_MIRROR = 0x141; // lane i <-> 7-i within 8: flip bits 0..2
+constexpr int DPP_MIRROR = 0x140;      // lane i <-> 15-i within 16: flip bits 0..3
+
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// a' = a with rows {1,3} (lanes 16-31, 48-63) replaced by b's rows {0,2};
+// b' = b with rows {0,2} replaced by a's rows {1,3}.  Returns a' + b'.
+__device__ __forceinline__ double swap16_add(double a, double b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)ua, (uint32_t)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+  const double a2 = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+  const double b2 = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  return a2 + b2;
+}
+// same across the two 32-lane halves
+__device__ __forceinline__ double swap32_add(double a, double b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)ua, (uint32_t)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+  const double a2 = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+  const double b2 = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  return a2 + b2;
 }
 
+// butterfly sum over the wave; every lane ends with the bitwise-identical value
+__device__ __forceinline__ double wave_sum(double x) {
+  x += dpp<DPP_XOR1>(x);
+  x += dpp<DPP_XOR2>(x);
+  x += dpp<DPP_HALF_MIRROR>(x);
+  x += dpp<DPP_MIRROR>(x);
+  x = swap16_add(x, x);
+  return swap32_add(x, x);
+}
 __device__ __forceinline__ void wave_sum2(double& a, double& b) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    a += __shfl_xor(a, m);
-    b += __shfl_xor(b, m);
-  }
+  a += dpp<DPP_XOR1>(a);
+  b += dpp<DPP_XOR1>(b);
+  a += dpp<DPP_XOR2>(a);
+  b += dpp<DPP_XOR2>(b);
+  a += dpp<DPP_HALF_MIRROR>(a);
+  b += dpp<DPP_HALF_MIRROR>(b);
+  a += dpp<DPP_MIRROR>(a);
+  b += dpp<DPP_MIRROR>(b);
+  a = swap16_add(a, a);
+  b = swap16_add(b, b);
+  a = swap32_add(a, a);
+  b = swap32_add(b, b);
 }
 
 __device__ __forceinline__ double lse(double a, double b) {
@@ -103,9 +168,10 @@ __device__ __forceinline__ void normal_pair(RngKey k, uint32_t c0, uint32_t c1, 
   U4 r = philox4x32_10(c, k.k0, k.k1);
   const double u1 = u53(r.x, r.y), u2 = u53(r.z, r.w);
   const double rad = sqrt(-2.0 * log(1.0 - u1));
-  const double ang = 6.283185307179586 * u2;
-  n0 = rad * cos(ang);
-  n1 = rad * sin(ang);
+  double sn, cs;
+  sincospi(2.0 * u2, &sn, &cs);   // angle 2*pi*u2; sinpi/cospi need no Payne-Hanek reduction
+  n0 = rad * cs;
+  n1 = rad * sn;
 }
 
 // ---------------------------------------------------------------------------
@@ -117,9 +183,9 @@ template <> __device__ __forceinline__ double rcp_<double>(double x) {
   double e = fma(-x, r, 1.0);
   r = fma(r, e, r);
   e = fma(-x, r, 1.0);
-  r = fma(r, e, r);                             // two Newton steps: <= 1 ulp
+  r = fma(r, e, r);
   e = fma(-x, r, 1.0);
-  return fma(r, e, r);
+  return fma(r, e, r);                          // <= 1 ulp
 }
 template <> __device__ __forceinline__ float rcp_<float>(float x) {
   return __builtin_amdgcn_rcpf(x);
@@ -130,9 +196,8 @@ template <> __device__ __forceinline__ float exp_<float>(float x) { return __exp
 
 // Likelihood terms of one bin given its modulation dL (shared by every mode).
 // acc: [0] sum d^2, [1] sum a, [2] sum a e, [3] sum w; returns h (adjoint seed of dL).
-template <class R>
-__device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th3,
-                                      double (&acc)[NSLOT]) {
+template <class R, class A>
+__device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th3, A (&acc)[NSLOT]) {
   const R u = R(1) + dL;
   const R L = th3 * u;                                           // decay length theta3*(1+dL)
   const R iL = rcp_<R>(L);
@@ -142,80 +207,84 @@ __device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th
   const R a = d * isu;                                           // dlp/dm * sigma^2
   const R ae = a * e;
   const R w = ae * cx * iL;
-  acc[0] += (double)(d * d);
-  acc[1] += (double)a;
-  acc[2] += (double)ae;
-  acc[3] += (double)w;
-  if (!(u > R(0))) acc[0] = INFINITY;                            // non-physical decay length
+  acc[0] += (A)(d * d);
+  acc[1] += (A)a;
+  acc[2] += (A)ae;
+  acc[3] += (A)w;
+  if (!(u > R(0))) acc[0] = (A)INFINITY;                         // non-physical decay length
   return w * iL;                                                 // dlp/ddL / (th2 th3) * sigma^2
 }
 
 // MODE_POLY: dL = a P(t) with P = sum_l c_l t^l ; moments M_l += h a t^l
-template <class R, int NNP>
+template <class R, int NNP, class A>
 __device__ __forceinline__ void bin_poly(R cx, R y, R isu, R t, R av, R th1, R th2, R th3,
-                                         const R (&cf)[NNP], double (&acc)[NSLOT]) {
+                                         const R (&cf)[NNP], A (&acc)[NSLOT]) {
   R P = cf[NNP - 1];
 #pragma unroll
   for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
-  const R h = bin_core<R>(av * P, cx, y, isu, th1, th2, th3, acc);
+  const R h = bin_core<R, A>(av * P, cx, y, isu, th1, th2, th3, acc);
   R p = h * av;
-  acc[4] += (double)p;
+  acc[4] += (A)p;
 #pragma unroll
   for (int l = 1; l < NNP; ++l) {
     p *= t;
-    acc[4 + l] += (double)p;
+    acc[4 + l] += (A)p;
   }
 }
 
-// MODE_BREG / MODE_STREAM: dL = B_i . yGP ; (B^T h)_k += B_ik h
-template <class R, int NNP>
+// MODE_ROWS / MODE_STREAM: dL = B_i . yGP ; (B^T h)_k += B_ik h
+template <class R, int NNP, class A>
 __device__ __forceinline__ void bin_rows(R cx, R y, R isu, const R (&Brow)[NNP], R th1, R th2,
-                                         R th3, const R (&yg)[NNP], double (&acc)[NSLOT]) {
+                                         R th3, const R (&yg)[NNP], A (&acc)[NSLOT]) {
   R dL = R(0);
 #pragma unroll
   for (int k = 0; k < NNP; ++k) dL = fma(Brow[k], yg[k], dL);
-  const R h = bin_core<R>(dL, cx, y, isu, th1, th2, th3, acc);
+  const R h = bin_core<R, A>(dL, cx, y, isu, th1, th2, th3, acc);
 #pragma unroll
-  for (int k = 0; k < NNP; ++k) acc[4 + k] += (double)(Brow[k] * h);
+  for (int k = 0; k < NNP; ++k) acc[4 + k] = fma((A)Brow[k], (A)h, acc[4 + k]);
 }
 
-// One exchange step of the transposed butterfly: lanes with `MASK` set keep the
-// upper half of their H live values, send the lower half, and vice versa.
-template <int H, int MASK>
-__device__ __forceinline__ void tr_step(double (&v)[NSLOT], bool up) {
+// Transposed butterfly over the wave: 32 values x 64 lanes -> lane l holds the
+// full sum of value (l >> 1).  Each step halves the live values: lanes whose
+// step bit is set keep the upper half.  Bits 5 and 4 use the gfx950 permlane
+// swaps (no select needed), bits 3..1 DPP row mirrors (partner differs in the
+// step bit and below), the final pair a quad swap.
+template <int H, int CTRL>
+__device__ __forceinline__ void tr_dpp(double (&v)[NSLOT], bool up) {
 #pragma unroll
   for (int i = 0; i < H; ++i) {
     const double send = up ? v[i] : v[i + H];
     const double keep = up ? v[i + H] : v[i];
-    v[i] = keep + __shfl_xor(send, MASK);
+    v[i] = keep + dpp<CTRL>(send);
   }
 }
-// 32 values x 64 lanes -> lane l holds the full sum of value (l >> 1).
 __device__ __forceinline__ double transpose_reduce32(double (&v)[NSLOT], int lane) {
-  tr_step<16, 32>(v, (lane & 32) != 0);
-  tr_step<8, 16>(v, (lane & 16) != 0);
-  tr_step<4, 8>(v, (lane & 8) != 0);
-  tr_step<2, 4>(v, (lane & 4) != 0);
-  tr_step<1, 2>(v, (lane & 2) != 0);
-  return v[0] + __shfl_xor(v[0], 1);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = swap32_add(v[i], v[i + 16]);   // lanes >= 32 keep [16,32)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = swap16_add(v[i], v[i + 8]);     // odd rows keep [8,16)
+  tr_dpp<4, DPP_MIRROR>(v, (lane & 8) != 0);
+  tr_dpp<2, DPP_HALF_MIRROR>(v, (lane & 4) != 0);
+  tr_dpp<1, DPP_QREV>(v, (lane & 2) != 0);
+  return v[0] + dpp<DPP_XOR1>(v[0]);
 }
 
 // per-lane resident bin data
 template <class R, int BPT, int NNP, int MODE>
 struct Bins {
   static constexpr int NB = BPT > 0 ? BPT : 1;
-  static constexpr int NR = MODE == MODE_POLY ? 2 : (MODE == MODE_BREG ? NNP : 1);
+  static constexpr int NR = MODE == MODE_POLY ? 2 : NNP;
   R cx[NB], y[NB], isu[NB];
   R row[NB][NR];
   __device__ void load(const KParams& P, int tid) {
-    if constexpr (MODE != MODE_STREAM) {
+    if constexpr (BPT > 0) {
       const R* pcx = (const R*)P.cx;
       const R* py = (const R*)P.y;
       const R* pisu = (const R*)P.isu;
       const R* pB = (const R*)P.B;
 #pragma unroll
       for (int b = 0; b < BPT; ++b) {
-        const int i = tid + b * TPB;
+        const int i = tid + b * GT;
         cx[b] = pcx[i];
         y[b] = py[i];
         isu[b] = pisu[i];
@@ -227,67 +296,87 @@ struct Bins {
 };
 
 // LDS carve -----------------------------------------------------------------
+// [ K^-1 (KMAX x KMAX, row stride NNP) | b (KMAX) | MP[GMAX][MPW] | PART[NGW][G][NSLOT] |
+//   G x chain{ ChainScalars | NVEC vectors | SUMS[NSLOT] | AUX[NAUX] | levels[max_depth][NLVL] } ]
 template <int PPL>
 struct Lds {
   static constexpr int VLEN = WAVE * PPL;
-  static constexpr int CHAIN_BYTES =
-      (int)sizeof(ChainScalars) + (NVEC + 1) * VLEN * 8 + NSLOT * 8;
   static constexpr int KBYTES = (KMAX * KMAX + KMAX) * 8;
   static __host__ __device__ constexpr int head_bytes(int G) {
-    return KBYTES + (GMAX * MPW + NW * G * NSLOT) * 8;
+    return KBYTES + (GMAX * MPW + NGW * G * NSLOT) * 8;
   }
-  static __host__ __device__ constexpr int bytes(int G) { return head_bytes(G) + G * CHAIN_BYTES; }
+  static __host__ __device__ constexpr int chain_bytes(int max_depth) {
+    return (int)sizeof(ChainScalars) + (NVEC * VLEN + NSLOT + NAUX + max_depth * NLVL * VLEN) * 8;
+  }
+  static __host__ __device__ constexpr int bytes(int G, int max_depth) {
+    return head_bytes(G) + G * chain_bytes(max_depth);
+  }
   char* base;
-  int G;
-  __device__ double* kinv() const { return (double*)base; }               // [Nn][Nn]
-  __device__ double* bv() const { return (double*)base + KMAX * KMAX; }   // [Nn]
+  int G, cb;
+  __device__ double* kinv() const { return (double*)base; }
+  __device__ double* bv() const { return (double*)base + KMAX * KMAX; }
   __device__ double* mp(int c) const { return (double*)(base + KBYTES) + c * MPW; }
   __device__ double* part() const { return (double*)(base + KBYTES) + GMAX * MPW; }
-  __device__ char* chain(int c) const { return base + head_bytes(G) + c * CHAIN_BYTES; }
+  __device__ char* chain(int c) const { return base + head_bytes(G) + c * cb; }
   __device__ ChainScalars& cs(int c) const { return *(ChainScalars*)chain(c); }
   __device__ double* vecs(int c) const { return (double*)(chain(c) + sizeof(ChainScalars)); }
-  __device__ double* qs(int c) const { return vecs(c) + NVEC * VLEN; }
-  __device__ double* sums(int c) const { return qs(c) + VLEN; }
+  __device__ double* sums(int c) const { return vecs(c) + NVEC * VLEN; }
+  __device__ double* aux(int c) const { return sums(c) + NSLOT; }
+  __device__ double* lvls(int c) const { return aux(c) + NAUX; }
 };
 
+// The likelihood sweep of chains [cb, ce) of the tile (gradient waves only).
+// PART[wave][c][0 .. 4+NNP) receives this wave's partial sums of chain c.
 template <class R, int BPT, int NNP, int MODE>
 __device__ void gradient_pass(const KParams& P, const Bins<R, BPT, NNP, MODE>& bins,
-                              const double* mpall, double* part, const int* act, int nct,
+                              const double* mpall, double* part, const int* done, int cb, int ce,
                               int tid, int lane, int wave) {
-  for (int c = 0; c < nct; ++c) {
-    if (!act[c]) continue;   // wave-uniform (LDS broadcast)
+  for (int c = cb; c < ce; ++c) {
+    if (done[c]) continue;   // wave-uniform (LDS broadcast)
     const double* mp = mpall + c * MPW;
     const R th1 = (R)mp[0], th2 = (R)mp[1], th3 = (R)mp[2];
-    R cf[NNP];   // POLY: c_l = b_l (K^-1 yGP)_l ; otherwise yGP_k
+    R cf[NNP];   // POLY: c_l = b_l (K^-1 yGP)_l ; ROWS: yGP_k
 #pragma unroll
     for (int k = 0; k < NNP; ++k) cf[k] = (R)mp[4 + k];
     double acc[NSLOT];
 #pragma unroll
     for (int k = 0; k < NSLOT; ++k) acc[k] = 0.0;
-    if constexpr (MODE == MODE_POLY) {
+    if constexpr (BPT > 0 && MODE == MODE_POLY) {
 #pragma unroll
       for (int b = 0; b < BPT; ++b)
-        bin_poly<R, NNP>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0], bins.row[b][1], th1,
-                         th2, th3, cf, acc);
-    } else if constexpr (MODE == MODE_BREG) {
+        bin_poly<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
+                                 bins.row[b][1], th1, th2, th3, cf, acc);
+    } else if constexpr (BPT > 0) {
+      // the few bins of one lane accumulate in R, the lane totals in f64
+      R racc[NSLOT];
+#pragma unroll
+      for (int k = 0; k < NSLOT; ++k) racc[k] = R(0);
 #pragma unroll
       for (int b = 0; b < BPT; ++b)
-        bin_rows<R, NNP>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b], th1, th2, th3, cf, acc);
+        bin_rows<R, NNP, R>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b], th1, th2, th3, cf,
+                            racc);
+#pragma unroll
+      for (int k = 0; k < 4 + NNP; ++k) acc[k] = (double)racc[k];
     } else {
       const R* pcx = (const R*)P.cx;
       const R* py = (const R*)P.y;
       const R* pisu = (const R*)P.isu;
       const R* pB = (const R*)P.B;
-      for (int i = tid; i < P.n_pad; i += TPB) {
-        R row[NNP];
+      for (int i = tid; i < P.n_pad; i += GT) {
+        if constexpr (MODE == MODE_POLY) {
+          bin_poly<R, NNP, double>(pcx[i], py[i], pisu[i], pB[2 * (size_t)i], pB[2 * (size_t)i + 1],
+                                   th1, th2, th3, cf, acc);
+        } else {
+          R row[NNP];
 #pragma unroll
-        for (int k = 0; k < NNP; ++k) row[k] = pB[(size_t)i * NNP + k];
-        bin_rows<R, NNP>(pcx[i], py[i], pisu[i], row, th1, th2, th3, cf, acc);
+          for (int k = 0; k < NNP; ++k) row[k] = pB[(size_t)i * NNP + k];
+          bin_rows<R, NNP, double>(pcx[i], py[i], pisu[i], row, th1, th2, th3, cf, acc);
+        }
       }
     }
     const double r = transpose_reduce32(acc, lane);
     const int idx = lane >> 1;
-    if (!(lane & 1) && idx < 4 + NNP) part[(wave * nct + c) * NSLOT + idx] = r;
+    if (!(lane & 1) && idx < 4 + NNP) part[(wave * P.G + c) * NSLOT + idx] = r;
   }
 }
 
@@ -299,35 +388,39 @@ struct Vd {
   double a[PPL];
 };
 
-template <int PPL>
+template <int PPL, int NNP>
 struct Chain {
   using V = Vd<PPL>;
   static constexpr int VLEN = WAVE * PPL;
-  const KParams& P;
-  ChainScalars& S;
+  const KParams* pp;   // laundered once per action: no kernarg load is hoisted across actions
+  ChainScalars* Sp;
   double* Vb;
-  double* QS;
   double* SUMS;
+  double* AUX;   // [0,32): yGP ; [32,64): horseshoe lambda_j * tau
+  double* LV;    // [max_depth][NLVL][VLEN]
   double* MP;
   double* part;
-  double* stk;
+  double* pool;  // HBM [max_depth+1][NPOOL][VLEN]
   const double* Kinv;
   const double* bv;
   int lane, slot, lc, gid, nct;
   RngKey key;
 
   __device__ Chain(const KParams& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
-      : P(P_), S(L.cs(slot_)), Vb(L.vecs(slot_)), QS(L.qs(slot_)), SUMS(L.sums(slot_)),
-        MP(L.mp(slot_)), part(L.part()), Kinv(L.kinv()), bv(L.bv()), lane(lane_), slot(slot_),
-        lc(lc_), nct(nct_) {
-    gid = P.chain_offset + lc;
-    key = make_key(P.seed, (uint32_t)gid);
-    stk = P.stack ? P.stack + (size_t)lc * P.max_depth * NSTK * VLEN : nullptr;
+      : pp(&P_), Sp(&L.cs(slot_)), Vb(L.vecs(slot_)), SUMS(L.sums(slot_)), AUX(L.aux(slot_)),
+        LV(L.lvls(slot_)), MP(L.mp(slot_)), part(L.part()), Kinv(L.kinv()), bv(L.bv()),
+        lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
+    gid = Pr().chain_offset + lc;
+    key = make_key(Pr().seed, (uint32_t)gid);
+    pool = Pr().stack ? Pr().stack + (size_t)lc * (Pr().max_depth + 1) * NPOOL * VLEN : nullptr;
   }
 
+  __device__ __forceinline__ const KParams& Pr() const { return *pp; }
   __device__ __forceinline__ int idx(int s) const { return s * WAVE + lane; }
-  __device__ __forceinline__ bool ok(int s) const { return idx(s) < P.D; }
+  __device__ __forceinline__ bool ok(int s) const { return idx(s) < Pr().D; }
   __device__ __forceinline__ double* vec(int v) const { return Vb + v * VLEN; }
+  __device__ __forceinline__ const double* QS() const { return Vb + V_QS * VLEN; }
+  __device__ __forceinline__ const double* QE() const { return Vb + V_QE * VLEN; }
   __device__ __forceinline__ V ld(int v) const {
     V r;
 #pragma unroll
@@ -338,29 +431,26 @@ struct Chain {
 #pragma unroll
     for (int s = 0; s < PPL; ++s) vec(v)[idx(s)] = x.a[s];
   }
-  __device__ __forceinline__ double* kslot(int level, int which) const {
-    return stk + ((size_t)level * NSTK + which) * VLEN;
+  __device__ __forceinline__ void copyv(int dst, int src) const { st(dst, ld(src)); }
+  __device__ __forceinline__ double* lvl(int level, int which) const {
+    return LV + ((size_t)level * NLVL + which) * VLEN;
   }
-  __device__ __forceinline__ V gld(int level, int which) const {
+  __device__ __forceinline__ V lld(int level, int which) const {
     V r;
-    const double* p = kslot(level, which);
+    const double* p = lvl(level, which);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) r.a[s] = p[idx(s)];
     return r;
   }
-  __device__ __forceinline__ void gst(int level, int which, const V& x) const {
-    double* p = kslot(level, which);
+  __device__ __forceinline__ void lst(int level, int which, const V& x) const {
+    double* p = lvl(level, which);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) p[idx(s)] = x.a[s];
   }
-  __device__ __forceinline__ void copyv(int dst, int src) const { st(dst, ld(src)); }
-
-  __device__ __forceinline__ double dot(const V& a, const V& b) const {
-    double x = 0.0;
-#pragma unroll
-    for (int s = 0; s < PPL; ++s) x = fma(a.a[s], b.a[s], x);
-    return wave_sum(x);
+  __device__ __forceinline__ double* pslot(int sl, int which) const {
+    return pool + ((size_t)sl * NPOOL + which) * VLEN;
   }
+
   __device__ __forceinline__ double kin(const V& p, const V& minv) const {
     double x = 0.0;
 #pragma unroll
@@ -379,91 +469,112 @@ struct Chain {
     wave_sum2(x, y);
     return x > 0.0 && y > 0.0;
   }
-  __device__ __forceinline__ bool is_log(int k) const { return k < 3 || k >= 3 + P.Nn; }
+  __device__ __forceinline__ bool is_log(int k) const { return k < 3 || k >= 3 + Pr().Nn; }
 
-  // ---------------- model parameters for the gradient phase ----------------
-  __device__ __forceinline__ double hs_lam(int j) const {
-    return exp(QS[5 + P.Nn + j] + 0.5 * QS[5 + 2 * P.Nn + j]);
-  }
-  __device__ __forceinline__ double hs_tau() const { return exp(QS[3 + P.Nn] + 0.5 * QS[4 + P.Nn]); }
-
+  // ---------------- the point handed to the gradient phase ------------------
+  // Stages q, caches its constrained values (QE) and, per family, yGP and the
+  // horseshoe scales (AUX), then writes the gradient phase's parameters MP:
+  // theta[3] and, per basis mode, yGP (rows) or c = b .* K^-1 yGP (poly).
   __device__ void write_mp(const V& q) const {
+    const int Nn = Pr().Nn;
+    double* qs = vec(V_QS);
+    double* qe = vec(V_QE);
 #pragma unroll
-    for (int s = 0; s < PPL; ++s) QS[idx(s)] = q.a[s];
-    wave_fence();
-    if (lane < MPW) {
-      double v = 0.0;
-      if (lane < 3) {
-        v = exp(QS[lane]);
-      } else if (lane >= 4 && lane - 4 < P.Nn) {
-        const int j = lane - 4;
-        v = (P.family == FAM_HORSESHOE) ? QS[3 + j] * hs_lam(j) * hs_tau() : QS[3 + j];
-      }
-      MP[lane] = v;
+    for (int s = 0; s < PPL; ++s) {
+      const int k = idx(s);
+      qs[k] = q.a[s];
+      qe[k] = (k < Pr().D && is_log(k)) ? exp(q.a[s]) : q.a[s];
     }
-    if (P.mode == MODE_POLY) {  // c_l = b_l (K^-1 yGP)_l
-      wave_fence();
-      const int Nn = P.Nn;
-      double c = 0.0;
+    wave_fence();
+    if (lane < NNP) {
+      double yv = 0.0, hl = 0.0;
       if (lane < Nn) {
-        for (int k = 0; k < Nn; ++k) c = fma(Kinv[lane * Nn + k], MP[4 + k], c);
-        c *= bv[lane];
+        if (Pr().family == FAM_HORSESHOE) {
+          // Tests/horseShoePrior.stan:30-32
+          hl = qe[5 + Nn + lane] * sqrt(qe[5 + 2 * Nn + lane]) * (qe[3 + Nn] * sqrt(qe[4 + Nn]));
+          yv = qs[3 + lane] * hl;
+        } else {
+          yv = qs[3 + lane];
+        }
       }
+      AUX[lane] = yv;
+      AUX[32 + lane] = hl;
+      if (Pr().mode != MODE_POLY) MP[4 + lane] = yv;
+    }
+    if (lane < 3) MP[lane] = qe[lane];
+    if (Pr().mode == MODE_POLY) {  // c_l = b_l (K^-1 yGP)_l ; K^-1 padded to NNP x NNP
       wave_fence();
-      if (lane < Nn) MP[4 + lane] = c;
+      if (lane < NNP) {
+        double c = 0.0;
+#pragma unroll
+        for (int k = 0; k < NNP; ++k) c = fma(Kinv[lane * NNP + k], AUX[k], c);
+        MP[4 + lane] = c * bv[lane];
+      }
     }
   }
 
   // ------------- lp / grad completion from the reduced bin sums --------------
+  __device__ void gather_sums() const {
+    if (Pr().prior_PD == 0) {
+      double s = 0.0;
+      if (lane < 4 + NNP) {
+#pragma unroll
+        for (int w = 0; w < NGW; ++w) s += part[(w * Pr().G + slot) * NSLOT + lane];
+      }
+      if (Pr().mode == MODE_POLY) {  // B^T h = K^-1 (b .* M)
+        if (lane >= 4 && lane < 4 + NNP) SUMS[lane] = s * bv[lane - 4];
+        else if (lane < 4) SUMS[lane] = s;
+        wave_fence();
+        if (lane < NNP) {
+          double v = 0.0;
+#pragma unroll
+          for (int l = 0; l < NNP; ++l) v = fma(Kinv[lane * NNP + l], SUMS[4 + l], v);
+          s = v;
+        }
+        wave_fence();
+        if (lane < NNP) SUMS[4 + lane] = s;
+      } else if (lane < 4 + NNP) {
+        SUMS[lane] = s;
+      }
+    }
+    wave_fence();
+  }
+
   __device__ double complete(V& g) const {
-    const int D = P.D, Nn = P.Nn, fam = P.family;
-    const bool lik = (P.prior_PD == 0);
+    const int D = Pr().D, Nn = Pr().Nn, fam = Pr().family;
+    const double* qs = QS();
+    const double* qe = QE();
+    const bool lik = (Pr().prior_PD == 0);
     const double Sd2 = SUMS[0];
     const bool bad = lik && !(Sd2 <= DBL_MAX);
-    const double u0 = QS[0], u1 = QS[1], u2 = QS[2];
-    const double th0 = exp(u0), th1 = exp(u1), th2 = exp(u2);
-    const double usig = QS[D - 1], sig = exp(usig), is2 = 1.0 / (sig * sig);
-    const double d0 = th0 - P.theta0[0], d1 = th1 - P.theta0[1], d2 = th2 - P.theta0[2];
-    const double* Si = P.S0inv;
+    const double th0 = qe[0], th1 = qe[1], th2 = qe[2];
+    const double usig = qs[D - 1], sig = qe[D - 1], is2 = 1.0 / (sig * sig);
+    const double d0 = th0 - Pr().theta0[0], d1 = th1 - Pr().theta0[1], d2 = th2 - Pr().theta0[2];
+    const double* Si = Pr().S0inv;
     const double Sd0 = Si[0] * d0 + Si[1] * d1 + Si[2] * d2;
     const double Sd1 = Si[3] * d0 + Si[4] * d1 + Si[5] * d2;
     const double Sd2t = Si[6] * d0 + Si[7] * d1 + Si[8] * d2;
-    const double ss = P.sigma_scale;
+    const double ss = Pr().sigma_scale;
     const double gyf = lik ? th1 * th2 * is2 : 0.0;   // dlp/dyGP_k = gyf * SUMS[4+k]
-    double lpc = 0.0;
+    double lpc = 0.0, lpc2 = 0.0;
     if (lane == 0) {
-      if (lik) lpc += -0.5 * Sd2 * is2 - (double)P.N * usig;
-      lpc += -0.5 * (d0 * Sd0 + d1 * Sd1 + d2 * Sd2t) + u0 + u1 + u2;
+      if (lik) lpc += -0.5 * Sd2 * is2 - (double)Pr().N * usig;
+      lpc += -0.5 * (d0 * Sd0 + d1 * Sd1 + d2 * Sd2t) + qs[0] + qs[1] + qs[2];
       lpc += -0.5 * (sig / ss) * (sig / ss) + usig;
     }
-    double lam = 0.0, S2 = 0.0, tau = 0.0, SGy = 0.0;
-    if (fam == FAM_NORMAL) {
-      lam = exp(QS[3 + Nn]);
-      double part_ = 0.0;
-#pragma unroll
-      for (int s = 0; s < PPL; ++s) {
-        const int k = idx(s);
-        if (k >= 3 && k < 3 + Nn) part_ += QS[k] * QS[k];
-      }
-      S2 = wave_sum(part_);
-    } else if (fam == FAM_HORSESHOE) {
-      tau = hs_tau();
-      double part_ = 0.0;
-#pragma unroll
-      for (int s = 0; s < PPL; ++s) {
-        const int k = idx(s);
-        if (k >= 3 && k < 3 + Nn) {
-          const int j = k - 3;
-          part_ += gyf * SUMS[4 + j] * (QS[k] * hs_lam(j) * tau);
-        }
-      }
-      SGy = wave_sum(part_);
+    // family-wide sums: normal sum yGP^2 ; horseshoe sum_j G_j yGP_j
+    if (lane < Nn) {
+      const double yv = AUX[lane];
+      lpc2 = (fam == FAM_HORSESHOE) ? gyf * SUMS[4 + lane] * yv : yv * yv;
     }
+    double famsum = lpc2;
+    if (fam != FAM_LASSO) famsum = wave_sum(lpc2);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
       double gk = 0.0;
       if (k < D) {
+        const double qk = qs[k];
         if (k < 3) {
           double gl = 0.0;
           if (lik) gl = (k == 0) ? SUMS[1] * is2 : (k == 1) ? SUMS[2] * is2 : th1 * SUMS[3] * is2 / th2;
@@ -471,50 +582,45 @@ struct Chain {
           const double sdk = (k == 0) ? Sd0 : (k == 1) ? Sd1 : Sd2t;
           gk = thk * (gl - sdk) + 1.0;
         } else if (k == D - 1) {
-          const double gl = lik ? (Sd2 * is2 - (double)P.N) / sig : 0.0;
+          const double gl = lik ? (Sd2 * is2 - (double)Pr().N) / sig : 0.0;
           gk = sig * (gl - sig / (ss * ss)) + 1.0;
         } else if (fam == FAM_NORMAL) {
+          const double lam = qe[3 + Nn];
           if (k < 3 + Nn) {
-            const double yv = QS[k];
-            gk = gyf * SUMS[4 + (k - 3)] - yv / (lam * lam);
-            lpc += -yv * yv / (2.0 * lam * lam);
-          } else {
-            const double rate = P.lambda_rate_eff;
-            gk = lam * (-(double)Nn / lam + S2 / (lam * lam * lam) - rate) + 1.0;
-            lpc += -(double)Nn * QS[k] - rate * lam + QS[k];
+            gk = gyf * SUMS[4 + (k - 3)] - qk / (lam * lam);
+            lpc += -qk * qk / (2.0 * lam * lam);
+          } else {  // lambda
+            const double rate = Pr().lambda_rate_eff;
+            gk = lam * (-(double)Nn / lam + famsum / (lam * lam * lam) - rate) + 1.0;
+            lpc += -(double)Nn * qk - rate * lam + qk;
           }
         } else if (fam == FAM_LASSO) {
-          const double yv = QS[k], ls = P.lambda_scale;
-          const double sg = (yv > 0.0) ? 1.0 : (yv < 0.0) ? -1.0 : 0.0;
-          gk = gyf * SUMS[4 + (k - 3)] - ls * sg - 2.0 * ls * yv;
-          lpc += -ls * fabs(yv) - ls * yv * yv;
+          const double ls = Pr().lambda_scale;
+          const double sg = (qk > 0.0) ? 1.0 : (qk < 0.0) ? -1.0 : 0.0;
+          gk = gyf * SUMS[4 + (k - 3)] - ls * sg - 2.0 * ls * qk;
+          lpc += -ls * fabs(qk) - ls * qk * qk;
         } else {  // horseshoe (Tests/horseShoePrior.stan:25-43)
-          const double nu = P.nu;
+          const double nu = Pr().nu, ek = qe[k];
           if (k < 3 + Nn) {
             const int j = k - 3;
-            const double z = QS[k];
-            gk = gyf * SUMS[4 + j] * hs_lam(j) * tau - z;
-            lpc += -0.5 * z * z;
+            gk = gyf * SUMS[4 + j] * AUX[32 + j] - qk;
+            lpc += -0.5 * qk * qk;
           } else if (k == 3 + Nn) {
-            const double r1 = exp(QS[k]);
-            gk = SGy - r1 * r1 + 1.0;
-            lpc += -0.5 * r1 * r1 + QS[k];
+            gk = famsum - ek * ek + 1.0;
+            lpc += -0.5 * ek * ek + qk;
           } else if (k == 4 + Nn) {
-            const double r2 = exp(QS[k]);
-            gk = 0.5 * SGy - 1.5 + 0.5 / r2 + 1.0;
-            lpc += -1.5 * QS[k] - 0.5 / r2 + QS[k];
+            gk = 0.5 * famsum - 1.5 + 0.5 / ek + 1.0;
+            lpc += -1.5 * qk - 0.5 / ek + qk;
           } else if (k < 5 + 2 * Nn) {
             const int j = k - 5 - Nn;
-            const double Gy = gyf * SUMS[4 + j] * (QS[3 + j] * hs_lam(j) * tau);
-            const double r1 = exp(QS[k]);
-            gk = Gy - r1 * r1 + 1.0;
-            lpc += -0.5 * r1 * r1 + QS[k];
+            const double Gy = gyf * SUMS[4 + j] * AUX[j];
+            gk = Gy - ek * ek + 1.0;
+            lpc += -0.5 * ek * ek + qk;
           } else {
             const int j = k - 5 - 2 * Nn;
-            const double Gy = gyf * SUMS[4 + j] * (QS[3 + j] * hs_lam(j) * tau);
-            const double r2 = exp(QS[k]);
-            gk = 0.5 * Gy - (0.5 * nu + 1.0) + 0.5 * nu / r2 + 1.0;
-            lpc += -(0.5 * nu + 1.0) * QS[k] - 0.5 * nu / r2 + QS[k];
+            const double Gy = gyf * SUMS[4 + j] * AUX[j];
+            gk = 0.5 * Gy - (0.5 * nu + 1.0) + 0.5 * nu / ek + 1.0;
+            lpc += -(0.5 * nu + 1.0) * qk - 0.5 * nu / ek + qk;
           }
         }
       }
@@ -523,25 +629,6 @@ struct Chain {
     double lp = wave_sum(lpc);
     if (bad || !(fabs(lp) <= DBL_MAX)) lp = -INFINITY;
     return lp;
-  }
-
-  __device__ void gather_sums() const {
-    if (P.prior_PD == 0 && lane < NSLOT) {
-      double s = 0.0;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) s += part[(w * nct + slot) * NSLOT + lane];
-      SUMS[lane] = s;
-    }
-    wave_fence();
-    if (P.prior_PD == 0 && P.mode == MODE_POLY) {  // B^T h = K^-1 (b .* M)
-      const int Nn = P.Nn;
-      double v = 0.0;
-      if (lane < Nn)
-        for (int l = 0; l < Nn; ++l) v = fma(Kinv[lane * Nn + l], bv[l] * SUMS[4 + l], v);
-      wave_fence();
-      if (lane < Nn) SUMS[4 + lane] = v;
-      wave_fence();
-    }
   }
 
   // ------------------------------ randomness --------------------------------
@@ -553,418 +640,445 @@ struct Chain {
       double n0, n1;
       normal_pair(key, c0, tag, (uint32_t)(k >> 1), c3, n0, n1);
       const double n = (k & 1) ? n1 : n0;
-      p.a[s] = (k < P.D) ? n / sqrt(minv.a[s]) : 0.0;
+      p.a[s] = (k < Pr().D) ? n / sqrt(minv.a[s]) : 0.0;
     }
     return p;
   }
 
-  // ------------------------------ init --------------------------------------
-  __device__ __attribute__((noinline)) void init_state() {
+  // =========================================================================
+  // The sampler as a flat action machine.  Every action appears once in the
+  // code and returns the next action; A_YIELD hands the position staged by
+  // A_WRITE_MP to the gradient waves.  Values crossing actions live in LDS.
+  // =========================================================================
+  enum Act : int {
+    A_YIELD = 0, A_GRAD, A_INIT_STATE, A_INIT_START, A_INIT_STEP, A_SS_BEGIN, A_SS_TRIAL,
+    A_SS_STEP, A_SS_FINISH, A_START_TRANSITION, A_BEGIN_SUBTREE, A_LEAF, A_END_TREE,
+    A_NEXT_TRANSITION, A_FINISH, A_LEAPFROG, A_WRITE_MP
+  };
+
+  __device__ __forceinline__ int uni(int x) const { return __builtin_amdgcn_readfirstlane(x); }
+
+  // a gradient arrived for CUR_Q: complete lp / grad, store them, dispatch
+  __device__ int act_grad() {
+    gather_sums();
+    V g;
+    const double lp = complete(g);
+    st(V_CUR_G, g);
+    Sp->cur_lp = lp;
+    Sp->cur_s2 = (Pr().prior_PD == 0) ? SUMS[0] : NAN;
+    const int stt = uni(Sp->state);
+    return stt == ST_TREE ? A_LEAF : stt == ST_STEPSIZE ? A_SS_STEP : A_INIT_STEP;
+  }
+
+  __device__ int act_init_state() {
     V one, zero;
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       one.a[s] = ok(s) ? 1.0 : 0.0;
       zero.a[s] = 0.0;
     }
+    Sp->prof[lane >> 5][lane & 31] = 0;
+#pragma unroll 1
+    for (int v = 0; v < NVEC; ++v) st(v, zero);
     st(V_MINV, one);
-    st(V_WF_M, zero);
-    st(V_WF_M2, zero);
-#pragma unroll
-    for (int v = 0; v < NVEC; ++v)
-      if (v != V_MINV && v != V_WF_M && v != V_WF_M2) st(v, zero);
     if (lane < NSLOT) SUMS[lane] = 0.0;
-    S.status = 0;
-    S.leapfrogs = 0;
-    S.eps = P.stepsize0;
-    S.mu = log(10.0 * P.stepsize0);
-    S.da_counter = 0;
-    S.s_bar = 0.0;
-    S.x_bar = 0.0;
+    AUX[lane] = 0.0;
+    Sp->status = 0;
+    Sp->leapfrogs = 0;
+    Sp->eps = Pr().stepsize0;
+    Sp->mu = log(10.0 * Pr().stepsize0);
+    Sp->da_counter = 0;
+    Sp->s_bar = 0.0;
+    Sp->x_bar = 0.0;
     // stan::mcmc::windowed_adaptation::set_window_params + restart
-    const int W = P.warmup;
-    int ib = P.init_buffer, tb = P.term_buffer, bw = P.base_window;
-    S.win_on = (W >= 20) ? 1 : 0;
+    const int W = Pr().warmup;
+    int ib = Pr().init_buffer, tb = Pr().term_buffer, bw = Pr().base_window;
+    Sp->win_on = (W >= 20) ? 1 : 0;
     if (W >= 20 && ib + bw + tb > W) {
       ib = (int)(0.15 * W);
       tb = (int)(0.1 * W);
       bw = W - (ib + tb);
     }
-    S.init_buf = ib;
-    S.term_buf = tb;
-    S.win_counter = 0;
-    S.win_size = bw;
-    S.win_next = ib + bw - 1;
-    S.wf_n = 0;
-    S.t = 0;
-    S.ss_window = 0;
-    S.depth = 0;
-    init_start(0);
+    Sp->init_buf = ib;
+    Sp->term_buf = tb;
+    Sp->win_counter = 0;
+    Sp->win_size = bw;
+    Sp->win_next = ib + bw - 1;
+    Sp->wf_n = 0;
+    Sp->t = 0;
+    Sp->ss_window = 0;
+    Sp->depth = 0;
+    Sp->pool_used = 0;
+    Sp->init_attempt = 0;
+    return A_INIT_START;
   }
 
-  __device__ void init_start(int attempt) {
-    const int Nn = P.Nn;
+  __device__ int act_init_start() {
+    const int Nn = Pr().Nn, attempt = uni(Sp->init_attempt);
     V q;
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
       double base = 0.0, w = 0.0;
       if (k < 3) {
-        base = log(P.theta0[k]);
+        base = log(Pr().theta0[k]);
         w = 0.025;
       } else if (k < 3 + Nn) {
         w = 0.05;
-      } else if (k < P.D) {
+      } else if (k < Pr().D) {
         w = 0.25;
-        if (P.family == FAM_NORMAL && k == 3 + Nn) base = -log(P.lambda_rate_eff);
+        if (Pr().family == FAM_NORMAL && k == 3 + Nn) base = -log(Pr().lambda_rate_eff);
       }
       const double u = uniform(key, (uint32_t)attempt, TAG_INIT, (uint32_t)k, 0u);
-      q.a[s] = (k < P.D) ? base + P.init_radius * w * (2.0 * u - 1.0) : 0.0;
+      q.a[s] = (k < Pr().D) ? base + Pr().init_radius * w * (2.0 * u - 1.0) : 0.0;
     }
     st(V_CUR_Q, q);
-    S.init_attempt = attempt;
-    S.state = ST_INIT;
-    write_mp(q);
+    Sp->state = ST_INIT;
+    return A_WRITE_MP;
   }
 
-  __device__ __attribute__((noinline)) void init_step(double lp, const V& g, double s2) {
+  __device__ int act_init_step() {
+    const V g = ld(V_CUR_G);
     double bad = 0.0;
 #pragma unroll
     for (int s = 0; s < PPL; ++s)
       if (ok(s) && !(fabs(g.a[s]) <= DBL_MAX)) bad = 1.0;
     bad = wave_sum(bad);
-    if (!(lp > -INFINITY) || bad != 0.0) {
-      if (S.init_attempt + 1 >= 100) {
-        S.status = ERR_INIT;
-        finish();
-        return;
+    if (!(Sp->cur_lp > -INFINITY) || bad != 0.0) {
+      if (Sp->init_attempt + 1 >= 100) {
+        Sp->status = ERR_INIT;
+        return A_FINISH;
       }
-      init_start(S.init_attempt + 1);
-      return;
+      Sp->init_attempt += 1;
+      return A_INIT_START;
     }
     copyv(V_SMP_Q, V_CUR_Q);
     st(V_SMP_G, g);
-    S.smp_lp = lp;
-    S.smp_s2 = s2;
-    if (P.adapt) {
-      ss_begin();
-    } else {
-      start_transition();
-    }
+    Sp->smp_lp = Sp->cur_lp;
+    Sp->smp_s2 = Sp->cur_s2;
+    return Pr().adapt ? A_SS_BEGIN : A_START_TRANSITION;
   }
 
   // --------------------- leapfrog (stan expl_leapfrog) -----------------------
-  __device__ void start_leapfrog(double e) {
+  // A_LEAPFROG: begin_update_p + update_q from CUR with step Sp->lf_e
+  __device__ int act_leapfrog() {
+    const double e = Sp->lf_e;
     V q = ld(V_CUR_Q), p = ld(V_CUR_P);
     const V g = ld(V_CUR_G), minv = ld(V_MINV);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
-      p.a[s] = fma(0.5 * e, g.a[s], p.a[s]);     // begin_update_p: p -= e/2 dphi/dq
-      q.a[s] = fma(e, minv.a[s] * p.a[s], q.a[s]);  // update_q: q += e M^-1 p
+      p.a[s] = fma(0.5 * e, g.a[s], p.a[s]);        // p -= e/2 dphi/dq
+      q.a[s] = fma(e, minv.a[s] * p.a[s], q.a[s]);  // q += e M^-1 p
     }
     st(V_CUR_P, p);
     st(V_CUR_Q, q);
-    write_mp(q);
+    return A_WRITE_MP;
   }
-  __device__ V finish_leapfrog(double e, const V& g) const {
+  __device__ int act_write_mp() {
+    write_mp(ld(V_CUR_Q));
+    return A_YIELD;
+  }
+  // end_update_p with the gradient that just arrived
+  __device__ V finish_leapfrog(double e) const {
     V p = ld(V_CUR_P);
+    const V g = ld(V_CUR_G);
 #pragma unroll
-    for (int s = 0; s < PPL; ++s) p.a[s] = fma(0.5 * e, g.a[s], p.a[s]);  // end_update_p
+    for (int s = 0; s < PPL; ++s) p.a[s] = fma(0.5 * e, g.a[s], p.a[s]);
     st(V_CUR_P, p);
-    st(V_CUR_G, g);
     return p;
   }
 
-  // ----------------- base_hmc::init_stepsize as a state machine --------------
-  __device__ void ss_begin() {
-    const double eps = S.eps;
-    if (eps == 0.0 || eps > 1e7 || isnan(eps)) {  // skipped like Stan
-      ss_finish();
-      return;
-    }
-    S.ss_trial = 0;
-    S.state = ST_STEPSIZE;
-    ss_new_trial();
+  // ----------------- base_hmc::init_stepsize as actions ----------------------
+  __device__ int act_ss_begin() {
+    const double eps = Sp->eps;
+    if (eps == 0.0 || eps > 1e7 || isnan(eps)) return A_SS_FINISH;  // skipped like Stan
+    Sp->ss_trial = 0;
+    Sp->state = ST_STEPSIZE;
+    return A_SS_TRIAL;
   }
-  __device__ void ss_new_trial() {
+  __device__ int act_ss_trial() {
     const V minv = ld(V_MINV);
-    const V p = momentum(TAG_SSMOM, (uint32_t)S.ss_window, (uint32_t)S.ss_trial, minv);
-    S.ss_H0 = -S.smp_lp + kin(p, minv);
+    const V p = momentum(TAG_SSMOM, (uint32_t)uni(Sp->ss_window), (uint32_t)uni(Sp->ss_trial), minv);
+    Sp->ss_H0 = -Sp->smp_lp + kin(p, minv);
     copyv(V_CUR_Q, V_SMP_Q);
     copyv(V_CUR_G, V_SMP_G);
     st(V_CUR_P, p);
-    start_leapfrog(S.eps);
+    Sp->lf_e = Sp->eps;
+    return A_LEAPFROG;
   }
-  __device__ __attribute__((noinline)) void ss_step(double lp, const V& g) {
-    const V p = finish_leapfrog(S.eps, g);
-    double h = -lp + kin(p, ld(V_MINV));
+  __device__ int act_ss_step() {
+    const V p = finish_leapfrog(Sp->eps);
+    double h = -Sp->cur_lp + kin(p, ld(V_MINV));
     if (isnan(h)) h = INFINITY;
-    const double dH = S.ss_H0 - h;
+    const double dH = Sp->ss_H0 - h;
     const double L08 = -0.22314355131420976;  // log(0.8)
-    if (S.ss_trial == 0) {
-      S.ss_dir = (dH > L08) ? 1 : -1;
-      S.ss_trial = 1;
-      ss_new_trial();
-      return;
+    if (Sp->ss_trial == 0) {
+      Sp->ss_dir = (dH > L08) ? 1 : -1;
+      Sp->ss_trial = 1;
+      return A_SS_TRIAL;
     }
-    if ((S.ss_dir == 1 && !(dH > L08)) || (S.ss_dir == -1 && !(dH < L08))) {
-      ss_finish();
-      return;
+    if ((Sp->ss_dir == 1 && !(dH > L08)) || (Sp->ss_dir == -1 && !(dH < L08))) return A_SS_FINISH;
+    Sp->eps = (Sp->ss_dir == 1) ? 2.0 * Sp->eps : 0.5 * Sp->eps;
+    if (Sp->eps > 1e7 || Sp->eps == 0.0 || Sp->ss_trial > 2000) {
+      Sp->status = ERR_NUMERIC;
+      return A_FINISH;
     }
-    S.eps = (S.ss_dir == 1) ? 2.0 * S.eps : 0.5 * S.eps;
-    if (S.eps > 1e7 || S.eps == 0.0 || S.ss_trial > 2000) {
-      S.status = ERR_NUMERIC;
-      finish();
-      return;
-    }
-    S.ss_trial += 1;
-    ss_new_trial();
+    Sp->ss_trial += 1;
+    return A_SS_TRIAL;
   }
-  __device__ void ss_finish() {
-    if (S.ss_window == 0) {
-      start_transition();
-    } else {  // adapt_diag_e_nuts::transition after a metric update
-      S.mu = log(10.0 * S.eps);
-      S.da_counter = 0;
-      S.s_bar = 0.0;
-      S.x_bar = 0.0;
-      next_transition();
-    }
+  __device__ int act_ss_finish() {
+    if (uni(Sp->ss_window) == 0) return A_START_TRANSITION;
+    // adapt_diag_e_nuts::transition after a metric update
+    Sp->mu = log(10.0 * Sp->eps);
+    Sp->da_counter = 0;
+    Sp->s_bar = 0.0;
+    Sp->x_bar = 0.0;
+    return A_NEXT_TRANSITION;
   }
 
   // ------------------------------ transition --------------------------------
-  __device__ void start_transition() {
-    S.state = ST_TREE;
-    S.eps_used = S.eps;
+  __device__ int act_start_transition() {
+    Sp->state = ST_TREE;
+    Sp->eps_used = Sp->eps;
     const V minv = ld(V_MINV);
-    const V p = momentum(TAG_MOM, (uint32_t)S.t, 0u, minv);
+    const V p = momentum(TAG_MOM, (uint32_t)uni(Sp->t), 0u, minv);
     st(V_SMP_P, p);
-    S.H0 = -S.smp_lp + kin(p, minv);
+    Sp->H0 = -Sp->smp_lp + kin(p, minv);
     const V q = ld(V_SMP_Q), g = ld(V_SMP_G);
     st(V_E0_Q, q); st(V_E0_P, p); st(V_E0_G, g);
     st(V_E1_Q, q); st(V_E1_P, p); st(V_E1_G, g);
-    S.end_lp[0] = S.end_lp[1] = S.smp_lp;
-    S.end_s2[0] = S.end_s2[1] = S.smp_s2;
+    Sp->end_lp[0] = Sp->end_lp[1] = Sp->smp_lp;
+    Sp->end_s2[0] = Sp->end_s2[1] = Sp->smp_s2;
     st(V_RHO, p);
-    S.lsw = 0.0;
-    S.n_leapfrog = 0;
-    S.sum_metro = 0.0;
-    S.depth = 0;
-    S.divergent = 0;
-    begin_subtree();
+    Sp->lsw = 0.0;
+    Sp->n_leapfrog = 0;
+    Sp->sum_metro = 0.0;
+    Sp->depth = 0;
+    Sp->divergent = 0;
+    Sp->pool_used = 0;
+    return A_BEGIN_SUBTREE;
   }
 
-  __device__ void begin_subtree() {
-    const int d = S.depth;
-    const double u = uniform(key, (uint32_t)S.t, TAG_DIR, (uint32_t)d, 0u);
+  __device__ int act_begin_subtree() {
+    const int d = uni(Sp->depth);
+    const double u = uniform(key, (uint32_t)uni(Sp->t), TAG_DIR, (uint32_t)d, 0u);
     const int dir = (u > 0.5) ? 1 : 0;
-    S.dir = dir;
+    Sp->dir = dir;
     const int eq = dir ? V_E1_Q : V_E0_Q;
     const V pe = ld(eq + 1);
     st(V_PNEAR, pe);
     copyv(V_CUR_Q, eq);
     st(V_CUR_P, pe);
     copyv(V_CUR_G, eq + 2);
-    S.cur_lp = S.end_lp[dir];
-    S.cur_s2 = S.end_s2[dir];
-    S.leaf = 0;
-    start_leapfrog(dir ? S.eps_used : -S.eps_used);
+    Sp->cur_lp = Sp->end_lp[dir];
+    Sp->cur_s2 = Sp->end_s2[dir];
+    Sp->leaf = 0;
+    Sp->lf_e = dir ? Sp->eps_used : -Sp->eps_used;
+    return A_LEAPFROG;
   }
 
-  __device__ void push(int l, const V& pb, const V& pe, const V& rho, double lsw, int prop) {
-    gst(l, K_PBEG, pb);
-    gst(l, K_PEND, pe);
-    gst(l, K_RHO, rho);
-    S.st_lsw[l] = lsw;
-    if (prop < 0) {
-      gst(l, K_PQ, ld(V_CUR_Q));
-      gst(l, K_PP, ld(V_CUR_P));
-      gst(l, K_PG, ld(V_CUR_G));
-      S.st_lp[l] = S.cur_lp;
-      S.st_s2[l] = S.cur_s2;
-    } else {
-      gst(l, K_PQ, gld(prop, K_PQ));
-      gst(l, K_PP, gld(prop, K_PP));
-      gst(l, K_PG, gld(prop, K_PG));
-      S.st_lp[l] = S.st_lp[prop];
-      S.st_s2[l] = S.st_s2[prop];
-    }
-  }
-
-  __device__ void take_sample(int prop) {
-    if (prop < 0) {
-      copyv(V_SMP_Q, V_CUR_Q);
-      copyv(V_SMP_P, V_CUR_P);
-      copyv(V_SMP_G, V_CUR_G);
-      S.smp_lp = S.cur_lp;
-      S.smp_s2 = S.cur_s2;
-    } else {
-      st(V_SMP_Q, gld(prop, K_PQ));
-      st(V_SMP_P, gld(prop, K_PP));
-      st(V_SMP_G, gld(prop, K_PG));
-      S.smp_lp = S.st_lp[prop];
-      S.smp_s2 = S.st_s2[prop];
-    }
-  }
-
-  // one leaf of base_nuts::build_tree, followed by every merge it completes
-  __device__ __attribute__((noinline)) void tree_leaf(double lp, const V& g, double s2) {
-    const double e = S.dir ? S.eps_used : -S.eps_used;
-    const V p = finish_leapfrog(e, g);
-    const V minv = ld(V_MINV);
-    S.cur_lp = lp;
-    S.cur_s2 = s2;
-    S.n_leapfrog += 1;
-    double h = -lp + kin(p, minv);
-    if (isnan(h)) h = INFINITY;
-    if (h - S.H0 > 1000.0) S.divergent = 1;
-    const double wl = S.H0 - h;
-    S.sum_metro += (wl > 0.0) ? 1.0 : exp(wl);
-
-    V Tpb = p, Tpe = p, Trho = p;
-    double Tlsw = wl;
-    int Tprop = -1;
-    bool valid = (S.divergent == 0);
-    const int d = S.depth, j = S.leaf;
-    if (valid) {
-      for (int l = 0; l < d; ++l) {
-        if (((j >> l) & 1) == 0) {
-          push(l, Tpb, Tpe, Trho, Tlsw, Tprop);
-          break;
-        }
-        const V Ipb = gld(l, K_PBEG), Ipe = gld(l, K_PEND), Irho = gld(l, K_RHO);
-        const double Ilsw = S.st_lsw[l];
-        const double lsw_sub = lse(Ilsw, Tlsw);
-        if (!(Tlsw > lsw_sub)) {
-          const double u = uniform(key, (uint32_t)S.t, TAG_MERGE | ((uint32_t)l << 8) | ((uint32_t)d << 16),
-                                   (uint32_t)j, 0u);
-          if (!(u < exp(Tlsw - lsw_sub))) Tprop = l;
-        }
-        V rsub, rx, ry;
+  // proposal pool: at most max_depth + 1 live slots (stack records + the running subtree)
+  __device__ int pool_put_cur() {   // persist the current leaf as a proposal (HBM, no wait)
+    const unsigned used = (unsigned)uni(Sp->pool_used);
+    const int sl = __builtin_ctz(~used);
+    Sp->pool_used = (int)(used | (1u << sl));
+    const V q = ld(V_CUR_Q), p = ld(V_CUR_P), g = ld(V_CUR_G);
 #pragma unroll
-        for (int s = 0; s < PPL; ++s) {
-          rsub.a[s] = Irho.a[s] + Trho.a[s];
-          rx.a[s] = Irho.a[s] + Tpb.a[s];
-          ry.a[s] = Trho.a[s] + Ipe.a[s];
-        }
-        const bool okc = crit(Ipb, Tpe, rsub, minv) && crit(Ipb, Tpb, rx, minv) &&
-                         crit(Ipe, Tpe, ry, minv);
-        Tpb = Ipb;
-        Trho = rsub;
-        Tlsw = lsw_sub;
-        if (!okc) {
-          valid = false;
-          break;
-        }
+    for (int s = 0; s < PPL; ++s) {
+      pslot(sl, P_Q)[idx(s)] = q.a[s];
+      pslot(sl, P_P)[idx(s)] = p.a[s];
+      pslot(sl, P_G)[idx(s)] = g.a[s];
+    }
+    Sp->pool_lp[sl] = Sp->cur_lp;
+    Sp->pool_s2[sl] = Sp->cur_s2;
+    return sl;
+  }
+  __device__ void pool_free(int sl) {
+    if (sl >= 0) Sp->pool_used = (int)((unsigned)Sp->pool_used & ~(1u << sl));
+  }
+
+  // one leaf of base_nuts::build_tree, followed by every merge it completes and,
+  // when the subtree of depth d is complete, the top-level merge of the transition
+  __device__ int act_leaf() {
+    const double e = Sp->lf_e;
+    const V p = finish_leapfrog(e);
+    const V minv = ld(V_MINV);
+    Sp->n_leapfrog += 1;
+    double h = -Sp->cur_lp + kin(p, minv);
+    if (isnan(h)) h = INFINITY;
+    if (h - Sp->H0 > 1000.0) Sp->divergent = 1;
+    const double wl = Sp->H0 - h;
+    Sp->sum_metro += (wl > 0.0) ? 1.0 : exp(wl);
+    if (uni(Sp->divergent)) return A_END_TREE;
+
+    V Tpb = p, Trho = p;
+    double Tlsw = wl;
+    int Tprop = -1;   // -1: the current leaf (CUR); else a pool slot
+    const int d = uni(Sp->depth), j = uni(Sp->leaf);
+    const uint32_t t = (uint32_t)uni(Sp->t);
+#pragma unroll 1
+    for (int l = 0; l < d; ++l) {
+      if (((j >> l) & 1) == 0) {   // push T as the init subtree of level l+1
+        lst(l, K_PBEG, Tpb);
+        lst(l, K_PEND, p);
+        lst(l, K_RHO, Trho);
+        Sp->st_lsw[l] = Tlsw;
+        Sp->st_prop[l] = (Tprop < 0) ? pool_put_cur() : Tprop;
+        break;
       }
-    }
-    if (!valid) {
-      end_tree();
-      return;
-    }
-    if (j == (1 << d) - 1) {  // the subtree of depth d is complete and valid
-      const int dir = S.dir;
-      const int eq = dir ? V_E1_Q : V_E0_Q;
-      copyv(eq, V_CUR_Q);
-      st(eq + 1, p);
-      st(eq + 2, g);
-      S.end_lp[dir] = S.cur_lp;
-      S.end_s2[dir] = S.cur_s2;
-      S.depth = d + 1;
-      bool take;
-      if (Tlsw > S.lsw) {
-        take = true;
+      // merge init I = level l with final T (base_nuts::build_tree at depth l+1)
+      const V Ipb = lld(l, K_PBEG), Ipe = lld(l, K_PEND), Irho = lld(l, K_RHO);
+      const double Ilsw = Sp->st_lsw[l];
+      const int Iprop = uni(Sp->st_prop[l]);
+      const double lsw_sub = lse(Ilsw, Tlsw);
+      bool take_final = true;
+      if (!(Tlsw > lsw_sub)) {
+        const double u = uniform(key, t, TAG_MERGE | ((uint32_t)l << 8) | ((uint32_t)d << 16),
+                                 (uint32_t)j, 0u);
+        take_final = u < exp(Tlsw - lsw_sub);
+      }
+      if (take_final) {
+        pool_free(Iprop);
       } else {
-        const double u = uniform(key, (uint32_t)S.t, TAG_TOP, (uint32_t)d, 0u);
-        take = u < exp(Tlsw - S.lsw);
+        pool_free(Tprop);
+        Tprop = Iprop;
       }
-      if (take) take_sample(Tprop);
-      S.lsw = lse(S.lsw, Tlsw);
-      const V far = ld(dir ? V_E0_P : V_E1_P), near = ld(V_PNEAR), rho = ld(V_RHO);
-      V rtot, rx, ry;
+      V rsub, rx, ry;
 #pragma unroll
       for (int s = 0; s < PPL; ++s) {
-        rtot.a[s] = rho.a[s] + Trho.a[s];
-        rx.a[s] = rho.a[s] + Tpb.a[s];
-        ry.a[s] = Trho.a[s] + near.a[s];
+        rsub.a[s] = Irho.a[s] + Trho.a[s];
+        rx.a[s] = Irho.a[s] + Tpb.a[s];
+        ry.a[s] = Trho.a[s] + Ipe.a[s];
       }
-      const bool persist = crit(far, Tpe, rtot, minv) && crit(far, Tpb, rx, minv) &&
-                           crit(near, Tpe, ry, minv);
-      st(V_RHO, rtot);
-      if (!persist || S.depth >= P.max_depth) {
-        end_tree();
-        return;
-      }
-      begin_subtree();
-    } else {
-      S.leaf = j + 1;
-      start_leapfrog(e);
+      const bool okc = crit(Ipb, p, rsub, minv) && crit(Ipb, Tpb, rx, minv) &&
+                       crit(Ipe, p, ry, minv);
+      Tpb = Ipb;
+      Trho = rsub;
+      Tlsw = lsw_sub;
+      if (!okc) return A_END_TREE;
     }
+    if (j != (1 << d) - 1) {
+      Sp->leaf = j + 1;
+      return A_LEAPFROG;
+    }
+    // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
+    const int dir = uni(Sp->dir);
+    const int eq = dir ? V_E1_Q : V_E0_Q;
+    copyv(eq, V_CUR_Q);
+    st(eq + 1, p);
+    copyv(eq + 2, V_CUR_G);
+    Sp->end_lp[dir] = Sp->cur_lp;
+    Sp->end_s2[dir] = Sp->cur_s2;
+    Sp->depth = d + 1;
+    bool take;
+    if (Tlsw > Sp->lsw) {
+      take = true;
+    } else {
+      const double u = uniform(key, t, TAG_TOP, (uint32_t)d, 0u);
+      take = u < exp(Tlsw - Sp->lsw);
+    }
+    if (take) {
+      if (Tprop < 0) {
+        copyv(V_SMP_Q, V_CUR_Q);
+        st(V_SMP_P, p);
+        copyv(V_SMP_G, V_CUR_G);
+        Sp->smp_lp = Sp->cur_lp;
+        Sp->smp_s2 = Sp->cur_s2;
+      } else {
+        V q2, p2, g2;
+#pragma unroll
+        for (int s = 0; s < PPL; ++s) {
+          q2.a[s] = pslot(Tprop, P_Q)[idx(s)];
+          p2.a[s] = pslot(Tprop, P_P)[idx(s)];
+          g2.a[s] = pslot(Tprop, P_G)[idx(s)];
+        }
+        st(V_SMP_Q, q2);
+        st(V_SMP_P, p2);
+        st(V_SMP_G, g2);
+        Sp->smp_lp = Sp->pool_lp[Tprop];
+        Sp->smp_s2 = Sp->pool_s2[Tprop];
+      }
+    }
+    pool_free(Tprop);
+    Sp->lsw = lse(Sp->lsw, Tlsw);
+    const V far = ld(dir ? V_E0_P : V_E1_P), near = ld(V_PNEAR), rho = ld(V_RHO);
+    V rtot, rx, ry;
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) {
+      rtot.a[s] = rho.a[s] + Trho.a[s];
+      rx.a[s] = rho.a[s] + Tpb.a[s];
+      ry.a[s] = Trho.a[s] + near.a[s];
+    }
+    const bool persist = crit(far, p, rtot, minv) && crit(far, Tpb, rx, minv) &&
+                         crit(near, p, ry, minv);
+    st(V_RHO, rtot);
+    if (!persist || d + 1 >= Pr().max_depth) return A_END_TREE;
+    return A_BEGIN_SUBTREE;
   }
 
   __device__ void write_draw(double accept, double energy) const {
-    const int t = S.t, W = P.warmup;
-    if (t < W && !P.save_warmup) return;
-    const int it = P.save_warmup ? t : t - W;
-    double* rec = P.draws + ((size_t)lc * P.iters_saved + it) * P.ncols;
+    const int t = Sp->t, W = Pr().warmup;
+    if (t < W && !Pr().save_warmup) return;
+    const int it = Pr().save_warmup ? t : t - W;
+    double* rec = Pr().draws + ((size_t)lc * Pr().iters_saved + it) * Pr().ncols;
     const V q = ld(V_SMP_Q);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
-      if (k < P.D) rec[7 + k] = is_log(k) ? exp(q.a[s]) : q.a[s];
+      if (k < Pr().D) rec[7 + k] = is_log(k) ? exp(q.a[s]) : q.a[s];
     }
     if (lane < 8) {
       double v;
       switch (lane) {
-        case 0: v = S.smp_lp; break;
+        case 0: v = Sp->smp_lp; break;
         case 1: v = accept; break;
-        case 2: v = S.eps_used; break;
-        case 3: v = (double)S.depth; break;
-        case 4: v = (double)S.n_leapfrog; break;
-        case 5: v = (double)S.divergent; break;
+        case 2: v = Sp->eps_used; break;
+        case 3: v = (double)Sp->depth; break;
+        case 4: v = (double)Sp->n_leapfrog; break;
+        case 5: v = (double)Sp->divergent; break;
         case 6: v = energy; break;
-        default: v = (P.prior_PD == 0) ? S.smp_s2 / (double)P.N : NAN; break;
+        default: v = (Pr().prior_PD == 0) ? Sp->smp_s2 / (double)Pr().N : NAN; break;
       }
-      rec[lane < 7 ? lane : 7 + P.D] = v;
+      rec[lane < 7 ? lane : 7 + Pr().D] = v;
     }
   }
 
-  __device__ void end_tree() {
-    const double accept = S.sum_metro / (double)S.n_leapfrog;
+  __device__ int act_end_tree() {
+    const double accept = Sp->sum_metro / (double)Sp->n_leapfrog;
     const V minv = ld(V_MINV);
-    const double energy = -S.smp_lp + kin(ld(V_SMP_P), minv);
+    const double energy = -Sp->smp_lp + kin(ld(V_SMP_P), minv);
     write_draw(accept, energy);
-    S.leapfrogs += S.n_leapfrog;
-    if (S.t < P.warmup && P.adapt) {
+    Sp->leapfrogs += Sp->n_leapfrog;
+    if (uni(Sp->t) < Pr().warmup && Pr().adapt) {
       learn_stepsize(accept);
       if (learn_variance()) {
-        S.ss_window += 1;
-        ss_begin();
-        return;
+        Sp->ss_window += 1;
+        return A_SS_BEGIN;
       }
     }
-    next_transition();
+    return A_NEXT_TRANSITION;
   }
 
   // stan::mcmc::stepsize_adaptation::learn_stepsize
   __device__ void learn_stepsize(double adapt_stat) {
-    S.da_counter += 1;
-    const double cnt = (double)S.da_counter;
+    Sp->da_counter += 1;
+    const double cnt = (double)Sp->da_counter;
     adapt_stat = adapt_stat > 1.0 ? 1.0 : adapt_stat;
-    const double eta = 1.0 / (cnt + P.t0);
-    S.s_bar = (1.0 - eta) * S.s_bar + eta * (P.adapt_delta - adapt_stat);
-    const double x = S.mu - S.s_bar * sqrt(cnt) / P.gamma;
-    const double x_eta = pow(cnt, -P.kappa);
-    S.x_bar = (1.0 - x_eta) * S.x_bar + x_eta * x;
-    S.eps = exp(x);
+    const double eta = 1.0 / (cnt + Pr().t0);
+    Sp->s_bar = (1.0 - eta) * Sp->s_bar + eta * (Pr().adapt_delta - adapt_stat);
+    const double x = Sp->mu - Sp->s_bar * sqrt(cnt) / Pr().gamma;
+    const double x_eta = pow(cnt, -Pr().kappa);
+    Sp->x_bar = (1.0 - x_eta) * Sp->x_bar + x_eta * x;
+    Sp->eps = exp(x);
   }
 
   // stan::mcmc::var_adaptation::learn_variance + windowed_adaptation
   __device__ bool learn_variance() {
-    const int W = P.warmup, cnt = S.win_counter;
-    const int tb = S.term_buf;
-    if (S.win_on && cnt >= S.init_buf && cnt < W - tb && cnt != W) {
-      S.wf_n += 1;
-      const double n = (double)S.wf_n;
+    const int W = Pr().warmup, cnt = uni(Sp->win_counter);
+    const int tb = Sp->term_buf;
+    if (Sp->win_on && cnt >= Sp->init_buf && cnt < W - tb && cnt != W) {
+      Sp->wf_n += 1;
+      const double n = (double)Sp->wf_n;
       const V q = ld(V_SMP_Q);
       V m = ld(V_WF_M), m2 = ld(V_WF_M2);
 #pragma unroll
@@ -976,18 +1090,18 @@ struct Chain {
       st(V_WF_M, m);
       st(V_WF_M2, m2);
     }
-    if (S.win_on && cnt == S.win_next && cnt != W) {
+    if (Sp->win_on && cnt == Sp->win_next && cnt != W) {
       // compute_next_window
       const int last = W - tb - 1;
-      if (S.win_next != last) {
-        S.win_size *= 2;
-        S.win_next = cnt + S.win_size;
-        if (S.win_next != last) {
-          const int boundary = S.win_next + 2 * S.win_size;
-          if (boundary >= W - tb) S.win_next = last;
+      if (Sp->win_next != last) {
+        Sp->win_size *= 2;
+        Sp->win_next = cnt + Sp->win_size;
+        if (Sp->win_next != last) {
+          const int boundary = Sp->win_next + 2 * Sp->win_size;
+          if (boundary >= W - tb) Sp->win_next = last;
         }
       }
-      const double n = (double)S.wf_n;
+      const double n = (double)Sp->wf_n;
       V var = ld(V_MINV);
       const V m2 = ld(V_WF_M2);
       V zero;
@@ -995,60 +1109,83 @@ struct Chain {
       for (int s = 0; s < PPL; ++s) {
         zero.a[s] = 0.0;
         if (ok(s)) {
-          if (S.wf_n > 1) var.a[s] = m2.a[s] / (n - 1.0);
+          if (Sp->wf_n > 1) var.a[s] = m2.a[s] / (n - 1.0);
           var.a[s] = (n / (n + 5.0)) * var.a[s] + 1e-3 * (5.0 / (n + 5.0));
         }
       }
       st(V_MINV, var);
       st(V_WF_M, zero);
       st(V_WF_M2, zero);
-      S.wf_n = 0;
-      S.win_counter = cnt + 1;
+      Sp->wf_n = 0;
+      Sp->win_counter = cnt + 1;
       return true;
     }
-    S.win_counter = cnt + 1;
+    Sp->win_counter = cnt + 1;
     return false;
   }
 
-  __device__ void next_transition() {
-    S.t += 1;
-    if (S.t == P.warmup && P.adapt && P.warmup > 0) S.eps = exp(S.x_bar);  // complete_adaptation
-    if (S.t >= P.warmup + P.samples) {
-      finish();
-      return;
-    }
-    start_transition();
+  __device__ int act_next_transition() {
+    Sp->t += 1;
+    const int t = uni(Sp->t);
+    if (t == Pr().warmup && Pr().adapt && Pr().warmup > 0) Sp->eps = exp(Sp->x_bar);  // complete_adaptation
+    if (t >= Pr().warmup + Pr().samples) return A_FINISH;
+    return A_START_TRANSITION;
   }
 
-  __device__ void finish() {
-    S.state = ST_DONE;
+  __device__ int act_finish() {
+    Sp->state = ST_DONE;
     const V q = ld(V_SMP_Q), minv = ld(V_MINV);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
-      if (k < P.D) {
-        if (P.fin_q) P.fin_q[(size_t)lc * P.D + k] = q.a[s];
-        if (P.fin_minv) P.fin_minv[(size_t)lc * P.D + k] = minv.a[s];
+      if (k < Pr().D) {
+        if (Pr().fin_q) Pr().fin_q[(size_t)lc * Pr().D + k] = q.a[s];
+        if (Pr().fin_minv) Pr().fin_minv[(size_t)lc * Pr().D + k] = minv.a[s];
       }
     }
     if (lane == 0) {
-      if (P.fin_eps) P.fin_eps[lc] = S.eps;
-      if (P.chain_status) P.chain_status[lc] = S.status;
-      if (P.leapfrogs) P.leapfrogs[lc] = S.leapfrogs;
+      if (Pr().fin_eps) Pr().fin_eps[lc] = Sp->eps;
+      if (Pr().chain_status) Pr().chain_status[lc] = Sp->status;
+      if (Pr().leapfrogs) Pr().leapfrogs[lc] = Sp->leapfrogs;
     }
+    return A_YIELD;
   }
 
-  // one NUTS phase: the gradient at CUR_Q is in the partial sums
-  __device__ __attribute__((noinline)) void phase() {
-    if (S.state == ST_DONE) return;
-    gather_sums();
-    V g;
-    const double lp = complete(g);
-    const double s2 = (P.prior_PD == 0) ? SUMS[0] : NAN;
-    switch (S.state) {
-      case ST_INIT: init_step(lp, g, s2); break;
-      case ST_STEPSIZE: ss_step(lp, g); break;
-      default: tree_leaf(lp, g, s2); break;
+  // run actions until the chain yields a position to the gradient waves (or finishes)
+  __device__ void run(int a) {
+    for (;;) {
+      a = uni(a);
+      // opaque per action: no jump threading across actions, and no address or
+      // kernarg load hoisted out of the action loop (keeps register pressure local)
+      asm volatile("" : "+s"(a), "+s"(pp));
+      if (a == A_YIELD) break;
+      const bool prof = Pr().stamps != nullptr;
+      const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
+      const int a0 = a;
+      switch (a) {
+        case A_GRAD: a = act_grad(); break;
+        case A_INIT_STATE: a = act_init_state(); break;
+        case A_INIT_START: a = act_init_start(); break;
+        case A_INIT_STEP: a = act_init_step(); break;
+        case A_SS_BEGIN: a = act_ss_begin(); break;
+        case A_SS_TRIAL: a = act_ss_trial(); break;
+        case A_SS_STEP: a = act_ss_step(); break;
+        case A_SS_FINISH: a = act_ss_finish(); break;
+        case A_START_TRANSITION: a = act_start_transition(); break;
+        case A_BEGIN_SUBTREE: a = act_begin_subtree(); break;
+        case A_LEAF: a = act_leaf(); break;
+        case A_END_TREE: a = act_end_tree(); break;
+        case A_NEXT_TRANSITION: a = act_next_transition(); break;
+        case A_FINISH: a = act_finish(); break;
+        case A_LEAPFROG: a = act_leapfrog(); break;
+        case A_WRITE_MP: a = act_write_mp(); break;
+        default: a = A_YIELD; break;
+      }
+      if (prof) {
+        wave_fence();
+        Sp->prof[0][a0] += (long long)__builtin_amdgcn_s_memtime() - t0;
+        Sp->prof[1][a0] += 1;
+      }
     }
     wave_fence();
   }
@@ -1057,94 +1194,188 @@ struct Chain {
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-template <int PPL>
+template <int PPL, int NNP>
 __device__ __forceinline__ void load_kinv(const KParams& P, const Lds<PPL>& L, int tid) {
-  if (P.mode == MODE_POLY) {
+  if (P.mode == MODE_POLY) {  // zero-padded to NNP x NNP so the device loops are fixed-size
     const int Nn = P.Nn;
-    for (int i = tid; i < Nn * Nn; i += TPB) L.kinv()[i] = P.Kinv[i];
-    if (tid < Nn) L.bv()[tid] = P.bvec[tid];
+    for (int i = tid; i < NNP * NNP; i += TPB) {
+      const int r = i / NNP, c = i % NNP;
+      L.kinv()[i] = (r < Nn && c < Nn) ? P.Kinv[r * Nn + c] : 0.0;
+    }
+    if (tid < NNP) L.bv()[tid] = (tid < Nn) ? P.bvec[tid] : 0.0;
+  }
+}
+
+// LDS hand-off primitives between the waves of one tile (one CU: LDS is a
+// single coherent memory, so a writer's ds ops completed under lgkmcnt(0) are
+// visible to every later read of any wave).
+__device__ __forceinline__ int lds_load(const int* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+__device__ __forceinline__ unsigned long long lds_load64(const unsigned long long* p) {
+  return __atomic_load_n(p, __ATOMIC_RELAXED);
+}
+constexpr int RINGN = 16;                 // hand-off ring: >= 2 * GMAX entries
+constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded, never hang a box
+
+// Dataflow pipeline inside a tile.  The NUTS wave of chain c writes the next
+// position's parameters to MP[c] and enqueues c in an LDS ring (64-bit entries
+// {sequence number, chain}); the gradient waves drain the ring in order, each
+// sweeping its bins for that chain and bumping grad_cnt[c]; the NUTS wave waits
+// until grad_cnt[c] reaches NGW * epoch and runs the sampler until it yields
+// the next position.  Chains cycle independently (no barrier after start-up),
+// so the sampler latency of one chain hides behind the sweeps of the others.
+template <class R, int BPT, int NNP, int PPL, int MODE>
+__global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict__ Pg) {
+  const KParams& P = *Pg;   // device-resident parameter block: uniform s_load reads
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const Lds<PPL> L{smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c0 = blockIdx.x * P.G;
+  const int nct = min(P.G, P.chains - c0);
+  __shared__ unsigned long long ring[RINGN];
+  __shared__ int q_reserve, n_active, grad_cnt[GMAX], pad_[2];
+
+  load_kinv<PPL, NNP>(P, L, tid);
+  if (tid == 0) {
+    q_reserve = 0;
+    n_active = nct;
+  }
+  if (tid < GMAX) grad_cnt[tid] = 0;
+  if (tid < RINGN) ring[tid] = ~0ULL;
+  __syncthreads();
+
+  const bool stamp = (P.stamps != nullptr) && lane == 0 && (wave == 0 || wave == NGW);
+  long long t_busy = 0, n_items = 0, t_begin = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  if (wave < NGW) {  // ------------------------- gradient waves
+    Bins<R, BPT, NNP, MODE> bins;
+    bins.load(P, tid);
+    int zero_done[GMAX] = {0, 0, 0, 0};
+    for (unsigned h = 0;; ++h) {
+      unsigned long long e;
+      bool stop = false;
+      long long spins = 0;
+      for (;;) {  // wait for ring entry h
+        e = lds_load64(&ring[h % RINGN]);
+        if ((unsigned)(e >> 32) == h) break;
+        if (lds_load(&n_active) == 0 || ++spins > SPIN_LIMIT) {
+          stop = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (stop) break;
+      const int c = (int)(e & 0xFF);
+      const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+      if (P.prior_PD == 0)
+        gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1, tid,
+                                         lane, wave);
+      wave_fence();   // this wave's PART writes are complete
+      if (lane == 0) atomicAdd(&grad_cnt[c], 1);
+      if (stamp) {
+        t_busy += (long long)__builtin_amdgcn_s_memtime() - s0;
+        ++n_items;
+      }
+    }
+  } else {           // ------------------------- NUTS waves
+    // the sampler is the latency-critical stage and shares each SIMD with two
+    // throughput-bound gradient waves: let it win issue arbitration
+    __builtin_amdgcn_s_setprio(3);
+    const int c = wave - NGW;
+    if (c < nct) {
+      Chain<PPL, NNP> ch(P, L, c, c0 + c, lane, nct);
+      long long epoch = 0;
+      int a = Chain<PPL, NNP>::A_INIT_STATE;
+      for (;;) {
+        const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+        ch.run(a);   // ends with the next position staged in MP[c] (or the chain done)
+        if (stamp) {
+          t_busy += (long long)__builtin_amdgcn_s_memtime() - s0;
+          ++n_items;
+        }
+        if (ch.Sp->state == ST_DONE) break;
+        if (epoch >= P.max_steps) {   // termination guarantee: report, never hang
+          ch.Sp->status = ERR_TIMEOUT;
+          ch.run(Chain<PPL, NNP>::A_FINISH);
+          break;
+        }
+        // enqueue chain c: sequence number from a ring-wide counter, one 64-bit store
+        if (lane == 0) {
+          const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
+          __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
+                           __ATOMIC_RELAXED);
+        }
+        ++epoch;
+        long long spins = 0;
+        while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
+          if (++spins > SPIN_LIMIT) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (spins > SPIN_LIMIT) {
+          ch.Sp->status = ERR_TIMEOUT;
+          ch.run(Chain<PPL, NNP>::A_FINISH);
+          break;
+        }
+        a = Chain<PPL, NNP>::A_GRAD;
+      }
+      wave_fence();
+      if (lane == 0) atomicSub(&n_active, 1);
+    }
+  }
+  if (stamp) {
+    long long* o = P.stamps + (size_t)blockIdx.x * 40;
+    if (wave == 0) {
+      o[0] = n_items;
+      o[1] = t_busy;
+      o[3] = (long long)__builtin_amdgcn_s_memtime() - t_begin;
+    } else {
+      o[2] = t_busy;
+      for (int k = 0; k < 18; ++k) {
+        o[4 + k] = L.cs(0).prof[0][k];
+        o[22 + k] = L.cs(0).prof[1][k];
+      }
+    }
   }
 }
 
 template <class R, int BPT, int NNP, int PPL, int MODE>
-__global__ void __launch_bounds__(TPB, 4) nuts_kernel(const KParams P) {
+__global__ void __launch_bounds__(TPB, 3) logp_kernel(const KParams* __restrict__ Pg) {
+  const KParams& P = *Pg;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds<PPL> L{smem, P.G};
-  const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid >> 6;
+  const Lds<PPL> L{smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c0 = blockIdx.x * P.G;
   const int nct = min(P.G, P.chains - c0);
-  __shared__ int act[GMAX];
-
-  Bins<R, BPT, NNP, MODE> bins;
-  bins.load(P, tid);
-  load_kinv(P, L, tid);
+  __shared__ int done[GMAX];
+  load_kinv<PPL, NNP>(P, L, tid);
+  if (tid < GMAX) done[tid] = tid >= nct;
   __syncthreads();
-
-  if (wave < nct) {
-    Chain<PPL> ch(P, L, wave, c0 + wave, lane, nct);
-    ch.init_state();
-    wave_fence();
-  }
-  __syncthreads();
-  const bool lik = (P.prior_PD == 0);
-  for (long long step = 0;; ++step) {
-    if (tid < GMAX) act[tid] = (tid < nct) && (L.cs(tid).state != ST_DONE);
-    __syncthreads();
-    int nact = 0;
-#pragma unroll
-    for (int c = 0; c < GMAX; ++c) nact += act[c];
-    if (nact == 0) break;
-    if (step >= P.max_steps) {  // termination guarantee: report and drain
-      if (wave < nct && lane == 0 && L.cs(wave).state != ST_DONE && P.chain_status)
-        P.chain_status[c0 + wave] = -6;
-      break;
-    }
-    if (lik)
-      gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), act, nct, tid, lane, wave);
-    __syncthreads();
-    if (wave < nct) {
-      Chain<PPL> ch(P, L, wave, c0 + wave, lane, nct);
-      ch.phase();
-    }
-    __syncthreads();
-  }
-}
-
-template <class R, int BPT, int NNP, int PPL, int MODE>
-__global__ void __launch_bounds__(TPB, 4) logp_kernel(const KParams P) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds<PPL> L{smem, P.G};
-  const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid >> 6;
-  const int c0 = blockIdx.x * P.G;
-  const int nct = min(P.G, P.chains - c0);
-  __shared__ int act[GMAX];
-  Bins<R, BPT, NNP, MODE> bins;
-  bins.load(P, tid);
-  load_kinv(P, L, tid);
-  if (tid < GMAX) act[tid] = (tid < nct);
-  __syncthreads();
-  if (wave < nct) {
-    Chain<PPL> ch(P, L, wave, c0 + wave, lane, nct);
+  const int c = wave - NGW;
+  if (wave >= NGW && c < nct) {
+    Chain<PPL, NNP> ch(P, L, c, c0 + c, lane, nct);
     Vd<PPL> q;
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = s * WAVE + lane;
-      q.a[s] = (k < P.D) ? P.q_in[(size_t)(c0 + wave) * P.D + k] : 0.0;
+      q.a[s] = (k < P.D) ? P.q_in[(size_t)(c0 + c) * P.D + k] : 0.0;
     }
     if (lane < NSLOT) ch.SUMS[lane] = 0.0;
     ch.write_mp(q);
     wave_fence();
   }
   __syncthreads();
-  if (P.prior_PD == 0)
-    gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), act, nct, tid, lane, wave);
+  if (wave < NGW && P.prior_PD == 0) {
+    Bins<R, BPT, NNP, MODE> bins;
+    bins.load(P, tid);
+    gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), done, 0, nct, tid, lane, wave);
+  }
   __syncthreads();
-  if (wave < nct) {
-    Chain<PPL> ch(P, L, wave, c0 + wave, lane, nct);
+  if (wave >= NGW && c < nct) {
+    Chain<PPL, NNP> ch(P, L, c, c0 + c, lane, nct);
     ch.gather_sums();
     Vd<PPL> g;
     const double lp = ch.complete(g);
-    const size_t pt = (size_t)(c0 + wave);
+    const size_t pt = (size_t)(c0 + c);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = s * WAVE + lane;
@@ -1160,54 +1391,56 @@ __global__ void __launch_bounds__(TPB, 4) logp_kernel(const KParams P) {
 // ---------------------------------------------------------------------------
 // host-side dispatch over the template grid
 // ---------------------------------------------------------------------------
-int lds_bytes(int ppl, int G) { return ppl == 1 ? Lds<1>::bytes(G) : Lds<2>::bytes(G); }
+int lds_bytes(int ppl, int G, int max_depth) {
+  return ppl == 1 ? Lds<1>::bytes(G, max_depth) : Lds<2>::bytes(G, max_depth);
+}
 
 template <class R, int BPT, int NNP, int PPL, int MODE>
-static hipError_t launch_t(bool logp, const KParams& P, int tiles, hipStream_t st) {
-  const int lds = Lds<PPL>::bytes(P.G);
+static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int tiles,
+                           hipStream_t st) {
+  const int lds = Lds<PPL>::bytes(P.G, P.max_depth);
   if (logp) {
     auto k = logp_kernel<R, BPT, NNP, PPL, MODE>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, P);
+    hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP);
   } else {
     auto k = nuts_kernel<R, BPT, NNP, PPL, MODE>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, P);
+    hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP);
   }
   return hipGetLastError();
 }
 
-template <int NNP, int PPL>
-static hipError_t launch_n(bool logp, bool mixed, int bpt, const KParams& P, int tiles,
+template <class R, int NNP, int PPL, int MODE>
+static hipError_t launch_m(bool logp, int bpt, const KParams& P, const KParams* dP, int tiles,
                            hipStream_t st) {
-  if (!mixed) {
-    if (P.mode == MODE_POLY) {
-      switch (bpt) {
-        case 1: return launch_t<double, 1, NNP, PPL, MODE_POLY>(logp, P, tiles, st);
-        case 2: return launch_t<double, 2, NNP, PPL, MODE_POLY>(logp, P, tiles, st);
-        case 4: return launch_t<double, 4, NNP, PPL, MODE_POLY>(logp, P, tiles, st);
-        default: return hipErrorInvalidValue;
-      }
-    }
-    return launch_t<double, 0, NNP, PPL, MODE_STREAM>(logp, P, tiles, st);
+  switch (bpt) {
+    case 0: return launch_t<R, 0, NNP, PPL, MODE>(logp, P, dP, tiles, st);
+    case 1: return launch_t<R, 1, NNP, PPL, MODE>(logp, P, dP, tiles, st);
+    case 2: return launch_t<R, 2, NNP, PPL, MODE>(logp, P, dP, tiles, st);
+    case 4: return launch_t<R, 4, NNP, PPL, MODE>(logp, P, dP, tiles, st);
+    default: return hipErrorInvalidValue;
   }
-  if (P.mode == MODE_BREG) {
-    switch (bpt) {
-      case 1: return launch_t<float, 1, NNP, PPL, MODE_BREG>(logp, P, tiles, st);
-      case 2: return launch_t<float, 2, NNP, PPL, MODE_BREG>(logp, P, tiles, st);
-      default: return hipErrorInvalidValue;
-    }
-  }
-  return launch_t<float, 0, NNP, PPL, MODE_STREAM>(logp, P, tiles, st);
 }
 
-hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P, int tiles,
-                  hipStream_t st) {
+template <int NNP, int PPL>
+static hipError_t launch_n(bool logp, bool mixed, int bpt, const KParams& P, const KParams* dP,
+                           int tiles, hipStream_t st) {
+  if (!mixed) {
+    if (P.mode == MODE_POLY) return launch_m<double, NNP, PPL, MODE_POLY>(logp, bpt, P, dP, tiles, st);
+    return launch_t<double, 0, NNP, PPL, MODE_ROWS>(logp, P, dP, tiles, st);
+  }
+  return launch_m<float, NNP, PPL, MODE_ROWS>(logp, bpt, P, dP, tiles, st);
+}
+
+// P: host copy (shapes); dP: the same block already copied to device memory
+hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P, const KParams* dP,
+                  int tiles, hipStream_t st) {
 #ifdef FITOCT_ONE_VARIANT
-  return launch_t<double, 2, 16, 1, MODE_POLY>(logp, P, tiles, st);
+  return launch_t<double, 4, 16, 1, MODE_POLY>(logp, P, dP, tiles, st);
 #else
-  if (nnp == 16) return launch_n<16, 1>(logp, mixed, bpt, P, tiles, st);
-  return launch_n<24, 2>(logp, mixed, bpt, P, tiles, st);
+  if (nnp == 16) return launch_n<16, 1>(logp, mixed, bpt, P, dP, tiles, st);
+  return launch_n<24, 2>(logp, mixed, bpt, P, dP, tiles, st);
 #endif
 }
 

@@ -26,7 +26,7 @@ for N, fam, Nn in [(512, "normal", 15), (2048, "horseshoe", 15), (4096, "lasso",
 
 d = synth_decay(2048, "sincExp", 1)
 prob = ExpGPProblem(d["x"], d["y"], d["uy"], Nn=15, gridType="extremal", theta0=t0, Sigma0=S0, prior_type="horseshoe")
-for C, W, S in [(4, 100, 100), (1024, 500, 1000)]:
+for C, W, S in [(4, 100, 100), (1024, 150, 150)]:
     cfg = SamplerConfig(chains=C, warmup=W, samples=S, seed=42)
     t = time.perf_counter()
     out = sample(prob, cfg)
