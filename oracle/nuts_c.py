@@ -1,0 +1,86 @@
+"""ORACLE (test infrastructure only) -- ctypes wrapper of oracle/build/liboracle.so,
+the C restatement of the ExpGP model and Stan's recursive NUTS (fitoct_oracle.c).
+
+Parity status vs rstan: **parity unpinned** (see fitoct_oracle.c header).
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+_L = None
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "fitoct_oracle.c")
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def lib():
+    global _L
+    if _L is None:
+        build()
+        from fitoct_amd import _lib as abi   # ABI struct layouts (include/fitoct.h)
+        L = C.CDLL(LIB)
+        dp = C.POINTER(C.c_double)
+        L.oracle_basis.argtypes = [C.POINTER(abi.Problem), dp]
+        L.oracle_logp_grad.argtypes = [C.POINTER(abi.Problem), C.c_int, dp, dp, dp, dp]
+        L.oracle_sample.argtypes = [C.POINTER(abi.Problem), C.POINTER(abi.Config), dp, dp, dp,
+                                    C.POINTER(C.c_longlong), C.c_int]
+        L.oracle_philox.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                    C.POINTER(C.c_uint32)]
+        _L = L
+    return _L
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    lib().oracle_philox(c, k, o)
+    return list(o)
+
+
+def basis(prob):
+    """prob: fitoct_amd.ExpGPProblem"""
+    B = np.zeros((prob.N, prob.Nn))
+    p = prob.to_c()
+    assert lib().oracle_basis(C.byref(p), _dp(B)) == 0
+    return B
+
+
+def logp_grad(prob, q):
+    q = np.ascontiguousarray(np.atleast_2d(q), dtype=np.float64)
+    P, D = q.shape
+    lp, g, s2 = np.zeros(P), np.zeros((P, D)), np.zeros(P)
+    p = prob.to_c()
+    assert lib().oracle_logp_grad(C.byref(p), P, _dp(q), _dp(lp), _dp(g), _dp(s2)) == 0
+    return lp, g, s2
+
+
+def sample(prob, cfg, nthreads: int = 0):
+    """prob: ExpGPProblem, cfg: SamplerConfig -> dict(draws, stepsize, inv_metric, leapfrogs)."""
+    D = prob.D
+    iters = cfg.warmup + cfg.samples if cfg.save_warmup else cfg.samples
+    draws = np.full((cfg.chains, iters, D + 8), np.nan)
+    eps = np.zeros(cfg.chains)
+    minv = np.zeros((cfg.chains, D))
+    lf = np.zeros(cfg.chains, dtype=np.int64)
+    p, c = prob.to_c(), cfg.to_c()
+    rc = lib().oracle_sample(C.byref(p), C.byref(c), _dp(draws), _dp(eps), _dp(minv),
+                             lf.ctypes.data_as(C.POINTER(C.c_longlong)), int(nthreads))
+    if rc != 0:
+        raise RuntimeError(f"oracle_sample failed with status {rc}")
+    return {"draws": draws, "stepsize": eps, "inv_metric": minv, "leapfrogs": lf}
