@@ -200,17 +200,19 @@ class Plan:
         check(lib().fitoct_plan_run(self._h, C.c_void_p(d_draws or None),
                                     C.c_void_p(stream or None)))
 
-    def download(self) -> SampleOutput:
+    def download(self, with_draws: bool = True) -> SampleOutput:
+        """Copy results to the host.  ``with_draws=False`` leaves the draws in HBM
+        (``SampleOutput.draws`` is None), e.g. when they are gathered over RCCL."""
         i = self.info
         C_, D = i["chains"], i["dim"]
-        draws = np.empty((C_, i["iters_saved"], i["n_cols"]))
+        draws = np.empty((C_, i["iters_saved"], i["n_cols"])) if with_draws else None
         eps = np.empty(C_)
         minv = np.empty((C_, D))
         lq = np.empty((C_, D))
         st = np.zeros(C_, dtype=np.int32)
         r = _lib.Result()
         r.draws = dptr(draws)
-        r.draws_capacity = draws.size
+        r.draws_capacity = draws.size if with_draws else 0
         r.stepsize, r.inv_metric, r.last_q = dptr(eps), dptr(minv), dptr(lq)
         r.chain_status = st.ctypes.data_as(C.POINTER(C.c_int32))
         check(lib().fitoct_plan_download(self._h, C.byref(r)))

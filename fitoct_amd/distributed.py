@@ -1,0 +1,99 @@
+"""Chain sharding across GPUs: one process per GPU, one RCCL gather of draws.
+
+SURVEY.md §8e: Stan chains adapt independently, so the chain set partitions
+with no data-path collective.  Rank r runs global chains
+``[offset_r, offset_r + count_r)``; each chain's random stream is keyed by
+(seed, global chain id) (fitoct_config.chain_offset), so the draws of chain c
+do not depend on how chains are split across ranks.  Every rank builds the GP
+basis from the same inputs (no broadcast).  At the end, one gather moves the
+draws to rank 0: with the ``nccl`` backend (RCCL over xGMI on MI355X) the draws
+never leave HBM before the gather; with ``gloo`` (CPU tests) they are host
+tensors.
+
+This replaces the reference's ``options(mc.cores = detectCores())`` chain
+parallelism of rstan (FitOCT.R:13, server.R:469).
+"""
+from __future__ import annotations
+
+from dataclasses import replace
+
+import numpy as np
+
+from .api import ExpGPProblem, Plan, SampleOutput, SamplerConfig
+
+
+def shard_range(total: int, world: int, rank: int):
+    """Contiguous block partition: (offset, count) of ``rank``'s chains."""
+    if not (0 <= rank < world) or total < 0:
+        raise ValueError("bad shard request")
+    base, rem = divmod(total, world)
+    count = base + (1 if rank < rem else 0)
+    offset = rank * base + min(rank, rem)
+    return offset, count
+
+
+def _gather_rows(t, world, rank, dst=0):
+    """Gather equal-shaped tensors to ``dst`` (list on dst, None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+    out = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
+    dist.gather(t, gather_list=out, dst=dst)
+    return out
+
+
+def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=None):
+    """Run ``cfg.chains`` global chains split over the process group; rank 0
+    returns the full :class:`SampleOutput` (chains in global order), other ranks
+    return their local output without draws.
+
+    ``engine(prob, local_cfg) -> SampleOutput`` runs one shard on the host side
+    (used with ``gloo``); with the ``nccl`` backend the HIP plan writes draws into
+    a device tensor that is gathered over RCCL directly.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    offset, count = shard_range(cfg.chains, world, rank)
+    cmax = -(-cfg.chains // world)
+    if count == 0:
+        raise ValueError(f"rank {rank} has no chains ({cfg.chains} chains over {world} ranks)")
+    local = replace(cfg, chains=count, chain_offset=cfg.chain_offset + offset)
+    nccl = dist.get_backend() == "nccl"
+    if nccl:
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        local = replace(local, device=dev.index)
+        with Plan(prob, local) as pl:
+            info = pl.info
+            iters, ncols = info["iters_saved"], info["n_cols"]
+            buf = torch.zeros((cmax, iters, ncols), dtype=torch.float64, device=dev)
+            pl.run(d_draws=buf.data_ptr(), stream=torch.cuda.current_stream(dev).cuda_stream)
+            out = pl.download(with_draws=False)
+    else:
+        if engine is None:
+            from .api import sample as engine
+        out = engine(prob, local)
+        iters, ncols = out.draws.shape[1:]
+        buf = torch.zeros((cmax, iters, ncols), dtype=torch.float64)
+        buf[:count] = torch.from_numpy(out.draws)
+        dev = torch.device("cpu")
+
+    # per-chain scalars ride along in one small tensor: [stepsize, leapfrogs(total), inv_metric, last_q]
+    D = out.inv_metric.shape[1]
+    meta = np.zeros((cmax, 2 + 2 * D))
+    meta[:count, 0] = out.stepsize
+    meta[0, 1] = out.total_leapfrogs
+    meta[:count, 2:2 + D] = out.inv_metric
+    meta[:count, 2 + D:] = out.last_q
+    meta_t = torch.from_numpy(meta).to(dev)
+    draws_all = _gather_rows(buf, world, rank)
+    meta_all = _gather_rows(meta_t, world, rank)
+    if rank != 0:
+        return out
+    counts = [shard_range(cfg.chains, world, r)[1] for r in range(world)]
+    draws = torch.cat([d[:n] for d, n in zip(draws_all, counts)]).cpu().numpy()
+    meta = torch.cat([m[:n] for m, n in zip(meta_all, counts)]).cpu().numpy()
+    total_lf = int(sum(float(m[0, 1]) for m in meta_all))
+    return SampleOutput(draws, prob.column_names(), out.warmup_saved, meta[:, 0].copy(),
+                        meta[:, 2:2 + D].copy(), meta[:, 2 + D:].copy(), total_lf,
+                        out.kernel_ms, out.wall_ms, cfg.chain_offset)

@@ -1,0 +1,114 @@
+"""Prior-only known-answer checks shared by the oracle tests (CPU) and the HIP
+sampler tests (GPU).  SURVEY.md §8c lists the analytic answers the reference's
+own files imply:
+
+(i)   Tests/testGamma.R:19-47 -- ``lambda ~ exponential(1/lambda_scale)``,
+      lambda_scale = 10, adapt_delta 0.99, max_treedepth 12: mean = sd = 10.
+      Here: normal family with ``prior_PD=1`` and ``lambda_rate=10`` (⚑
+      lambda_conv 0: rate = 1/lambda_rate), whose lambda marginal is exactly that
+      exponential (yGP ~ N(0, lambda) integrates out).
+(ii)  Tests/lassoPrior.stan:9-12 -- per-coordinate density
+      ``exp(-ls|y| - ls y^2)``; its variance by 1-D quadrature.
+(iii) Tests/horseShoePrior.stan:37-42 with nu = 1 -- z ~ N(0,1),
+      r1 ~ half-normal (median 0.6745), r2 ~ InvGamma(1/2,1/2) = 1/chi2_1
+      (median 2.198), so lambda_local, tau ~ half-Cauchy (median 1, q75 2.414).
+(iv)  ``prior_PD = 1`` (priPost.R:14): theta ~ N(theta0, Sigma0) (FitOCT.R:116-117),
+      sigma ~ half-normal(0, 10) (⚑ sigma prior): mean 7.979, sd 6.028.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+from scipy import integrate, stats
+
+from fitoct_amd import ExpGPProblem, SamplerConfig
+from fitoct_amd.synth import default_prior, synth_decay
+
+WARMUP, SAMPLES, CHAINS = 500, 2000, 8
+
+
+def lasso_sd(ls: float) -> float:
+    f = lambda y: math.exp(-ls * abs(y) - ls * y * y)           # noqa: E731
+    z = integrate.quad(f, -5, 5, points=[0.0])[0]
+    v = integrate.quad(lambda y: y * y * f(y), -5, 5, points=[0.0])[0]
+    return math.sqrt(v / z)
+
+
+def problem(family: str, Nn: int = 5, N: int = 64):
+    t0, S0 = default_prior()
+    d = synth_decay(N, "sincExp", 5)
+    kw = {"normal": dict(lambda_rate=10.0), "lasso": dict(lambda_scale=10.0),
+          "horseshoe": dict(nu=1.0)}[family]
+    return ExpGPProblem(d["x"], d["y"], d["uy"], Nn=Nn, gridType="extremal", theta0=t0,
+                        Sigma0=S0, prior_type=family, prior_PD=1, **kw)
+
+
+def config(seed=5, chains=CHAINS, warmup=WARMUP, samples=SAMPLES):
+    # testGamma.R:42-47 sampler controls
+    return SamplerConfig(chains=chains, warmup=warmup, samples=samples, seed=seed,
+                         adapt_delta=0.99, max_treedepth=12)
+
+
+def _mean_ok(x, truth, ess, sd_truth, k=4.5):
+    se = sd_truth / math.sqrt(max(ess, 1.0))
+    return abs(float(np.mean(x)) - truth) <= k * se, (float(np.mean(x)), truth, se)
+
+
+def check(family: str, draws: np.ndarray, columns: list, warmup: int, ess_fn):
+    """Return a list of failure strings (empty = pass).  draws[chain, iter, col]."""
+    post = draws[:, warmup:, :]
+    col = {c: i for i, c in enumerate(columns)}
+    fails = []
+
+    def mean_check(name, truth, sd_truth):
+        x = post[:, :, col[name]]
+        ok, info = _mean_ok(x, truth, ess_fn(x), sd_truth)
+        if not ok:
+            fails.append(f"{name}: mean {info[0]:.5g} vs {truth:.5g} (se {info[2]:.3g})")
+
+    def sd_check(name, truth, rtol):
+        s = float(np.std(post[:, :, col[name]]))
+        if abs(s - truth) > rtol * truth:
+            fails.append(f"{name}: sd {s:.5g} vs {truth:.5g}")
+
+    def quant_check(name, q, truth, rtol):
+        v = float(np.quantile(post[:, :, col[name]], q))
+        if abs(v - truth) > rtol * abs(truth):
+            fails.append(f"{name}: q{q} {v:.5g} vs {truth:.5g}")
+
+    t0, S0 = default_prior()
+    for k in range(3):
+        mean_check(f"theta.{k+1}", t0[k], math.sqrt(S0[k, k]))
+        sd_check(f"theta.{k+1}", math.sqrt(S0[k, k]), 0.06)
+    hn_mean, hn_sd = 10 * math.sqrt(2 / math.pi), 10 * math.sqrt(1 - 2 / math.pi)
+    mean_check("sigma", hn_mean, hn_sd)
+    sd_check("sigma", hn_sd, 0.06)
+    if family == "normal":
+        mean_check("lambda", 10.0, 10.0)
+        sd_check("lambda", 10.0, 0.15)
+        quant_check("lambda", 0.5, 10 * math.log(2), 0.08)
+    elif family == "lasso":
+        sd_t = lasso_sd(10.0)
+        for name in [c for c in columns if c.startswith("yGP.")]:
+            mean_check(name, 0.0, sd_t)
+            sd_check(name, sd_t, 0.05)
+    else:
+        zs = [c for c in columns if c.startswith("z.")]
+        for name in zs:
+            mean_check(name, 0.0, 1.0)
+            sd_check(name, 1.0, 0.05)
+        hn_med = stats.halfnorm.median()
+        ig_med = 1.0 / stats.chi2(1).median()
+        quant_check("r1_global", 0.5, hn_med, 0.06)
+        quant_check("r2_global", 0.5, ig_med, 0.10)
+        for k in range(len(zs)):
+            quant_check(f"r1_local.{k+1}", 0.5, hn_med, 0.06)
+            quant_check(f"r2_local.{k+1}", 0.5, ig_med, 0.10)
+        # lambda_local = r1*sqrt(r2) ~ half-Cauchy: P(lambda < 1) = 1/2, P(< tan(3pi/8)) = 3/4
+        lam = post[:, :, col["r1_local.1"]] * np.sqrt(post[:, :, col["r2_local.1"]])
+        for q, t in [(0.5, 1.0), (0.75, math.tan(3 * math.pi / 8))]:
+            v = float(np.quantile(lam, q))
+            if abs(v - t) > 0.08 * t:
+                fails.append(f"lambda_local.1 q{q} {v:.4g} vs {t:.4g}")
+    return fails

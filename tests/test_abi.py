@@ -1,0 +1,174 @@
+"""The drop-in boundary (include/fitoct.h) without a GPU: the library loads,
+exports every declared symbol, struct layouts agree with the ctypes mirror,
+host-side helpers (basis, names, diagnostics) agree with the oracles, and the
+error contract holds (negative status + message, no exception crossing the ABI).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden_files, load_golden, problems_from_fixture
+from fitoct_amd import _lib
+from fitoct_amd.api import ExpGPProblem, SamplerConfig
+from oracle import diag_np
+from oracle import model_np as M
+
+HEADER = os.path.join(ROOT, "include", "fitoct.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(fitoct_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 19
+    for s in syms:
+        assert hasattr(L, s), f"libfitoct.so does not export {s}"
+    assert sorted(n for n, _, _ in _lib.SIGNATURES) == syms
+
+
+def test_exports_are_c_linkage():
+    out = os.popen(f"nm -D --defined-only {_lib.LIB_PATH}").read()
+    exported = set(re.findall(r"\b(fitoct_[a-z0-9_]+)$", out, flags=re.M))
+    assert set(header_symbols()) <= exported
+
+
+def test_struct_layouts_match_ctypes():
+    sizes = _lib.struct_sizes()
+    assert sizes == (C.sizeof(_lib.Problem), C.sizeof(_lib.Config), C.sizeof(_lib.Result),
+                     C.sizeof(_lib.PlanInfo))
+    assert _lib.lib().fitoct_abi_version() == 1
+
+
+def test_default_config_is_stan_default():
+    c = _lib.Config()
+    _lib.lib().fitoct_default_config(C.byref(c))
+    assert (c.chains, c.warmup, c.samples, c.max_treedepth) == (4, 500, 1000, 10)
+    assert (c.adapt_delta, c.gamma, c.kappa, c.t0) == (0.8, 0.05, 0.75, 10.0)
+    assert (c.init_buffer, c.term_buffer, c.window) == (75, 50, 25)
+    assert c.init_radius == 2.0 and c.save_warmup == 1 and c.adapt_engaged == 1
+    p = _lib.Problem()
+    _lib.lib().fitoct_default_problem(C.byref(p))
+    assert list(p.theta0) == [1000.0, 2000.0, 300.0] and p.lambda_rate == 0.1
+    assert p.Sigma0[0] == pytest.approx(2500.0) and p.Sigma0[1] == 0.0
+
+
+@pytest.mark.parametrize("fam", ["normal", "lasso", "horseshoe"])
+@pytest.mark.parametrize("Nn", [5, 15, 24])
+def test_dims_and_column_names(fam, Nn):
+    code = _lib.PRIOR[fam]
+    L = _lib.lib()
+    D = M.dim(code, Nn)
+    assert L.fitoct_dim(code, Nn) == D
+    cols = _lib.column_names(code, Nn)
+    assert len(cols) == D + 8 == L.fitoct_n_cols(code, Nn)
+    assert cols[:7] == ["lp__", "accept_stat__", "stepsize__", "treedepth__", "n_leapfrog__",
+                        "divergent__", "energy__"]
+    # constrained parameters in model order, Stan's flattened naming (plotExpGP.R:41)
+    want = [n.replace("[", ".").replace("]", "") for n in M.param_names(code, Nn)]
+    assert cols[7:7 + D] == want and cols[-1] == "br"
+
+
+def test_column_name_errors():
+    buf = C.create_string_buffer(4)
+    L = _lib.lib()
+    assert L.fitoct_column_name(0, 5, 10_000, buf, 4) == -1
+    assert L.fitoct_column_name(0, 5, 1, buf, 4) == -1          # "accept_stat__" > 4 bytes
+    assert b"buffer" in L.fitoct_last_error()
+    assert L.fitoct_dim(7, 5) < 0
+
+
+@pytest.mark.parametrize("path", golden_files("logp"), ids=lambda p: os.path.basename(p))
+def test_build_basis_matches_oracle(path):
+    fx = load_golden(path)
+    prob, _ = problems_from_fixture(fx)
+    B, xg = prob.basis()
+    np.testing.assert_allclose(B, fx["B"], rtol=0, atol=1e-11)
+    np.testing.assert_allclose(xg, fx["xGP"], atol=1e-15)
+
+
+def _ar1(rng, chains, n, phi, shift=None):
+    x = np.zeros((chains, n))
+    e = rng.standard_normal((chains, n))
+    for t in range(1, n):
+        x[:, t] = phi * x[:, t - 1] + e[:, t]
+    if shift is not None:
+        x += np.asarray(shift)[:, None]
+    return x
+
+
+@pytest.mark.parametrize("case", ["iid", "ar1", "ar1_neg", "shifted", "short", "odd"])
+def test_split_rhat_ess_matches_restatement(case):
+    rng = np.random.Generator(np.random.PCG64(4))
+    x = {"iid": lambda: rng.standard_normal((4, 1000)),
+         "ar1": lambda: _ar1(rng, 4, 1000, 0.9),
+         "ar1_neg": lambda: _ar1(rng, 8, 500, -0.5),
+         "shifted": lambda: _ar1(rng, 4, 400, 0.3, shift=[0, 0, 0, 1.5]),
+         "short": lambda: rng.standard_normal((2, 20)),
+         "odd": lambda: _ar1(rng, 3, 301, 0.6)}[case]()
+    from fitoct_amd.stanfit import split_rhat_ess
+    r, e = split_rhat_ess(x)
+    assert r == pytest.approx(diag_np.split_rhat(x), rel=1e-10)
+    assert e == pytest.approx(diag_np.split_ess(x), rel=1e-8)
+
+
+def test_rank_rhat_detects_nonmixing():
+    from fitoct_amd.stanfit import rank_rhat
+    rng = np.random.Generator(np.random.PCG64(1))
+    good = rng.standard_normal((4, 500))
+    bad = good + np.array([0, 0, 0, 3.0])[:, None]
+    assert rank_rhat(good) < 1.01
+    assert rank_rhat(bad) > 1.1
+
+
+def test_problem_validation_before_device():
+    """Argument errors are reported as FITOCT_E_ARG even without a device."""
+    x = np.linspace(20, 500, 16)
+    prob = ExpGPProblem(x, x * 0 + 1000, x * 0 + 1.0, Nn=5)
+    prob.uy[3] = 0.0
+    with pytest.raises(_lib.FitOCTError) as ei:
+        from fitoct_amd.api import logp_grad
+        logp_grad(prob, np.zeros((1, prob.D)))
+    assert ei.value.code == -1 and "uy > 0" in str(ei.value)
+    prob.uy[3] = 1.0
+    prob.Nn = 30
+    p = prob.to_c()
+    assert _lib.lib().fitoct_build_basis(C.byref(p), None, None) == -1
+
+
+def test_config_validation():
+    from fitoct_amd.api import Plan
+    x = np.linspace(20, 500, 16)
+    prob = ExpGPProblem(x, x * 0 + 1000, x * 0 + 1.0, Nn=5)
+    for bad in [dict(chains=0), dict(samples=0), dict(max_treedepth=17), dict(adapt_delta=1.0),
+                dict(stepsize=0.0)]:
+        with pytest.raises(_lib.FitOCTError) as ei:
+            Plan(prob, SamplerConfig(**bad))
+        assert ei.value.code == -1
+
+
+@pytest.mark.skipif(_lib.lib().fitoct_device_count() > 0, reason="a GPU is visible")
+def test_no_device_fails_loudly():
+    """No CPU fallback: without a HIP device the sampler returns FITOCT_E_NODEVICE."""
+    x = np.linspace(20, 500, 16)
+    prob = ExpGPProblem(x, x * 0 + 1000, x * 0 + 1.0, Nn=5)
+    with pytest.raises(_lib.FitOCTError) as ei:
+        from fitoct_amd.api import sample
+        sample(prob, SamplerConfig(chains=1, warmup=5, samples=5))
+    assert ei.value.code == -3
+
+
+def test_missing_library_raises(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, "_LIB", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libfitoct.so"))
+    with pytest.raises(ImportError):
+        _lib.lib()

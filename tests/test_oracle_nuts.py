@@ -1,0 +1,90 @@
+"""C-oracle NUTS (oracle/fitoct_oracle.c): prior-only known answers, chain
+addressing (sharding invariance), determinism, and the committed draw fixtures.
+(CPU only -- these pin the checker that the GPU tests compare against.)
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import kat_cases as K
+from conftest import golden_files, load_golden
+from fitoct_amd import ExpGPProblem, SamplerConfig
+from oracle import diag_np, nuts_c
+
+
+@pytest.mark.parametrize("family", ["normal", "lasso", "horseshoe"])
+def test_prior_known_answers(family):
+    prob = K.problem(family)
+    cfg = K.config()
+    o = nuts_c.sample(prob, cfg, nthreads=8)
+    fails = K.check(family, o["draws"], prob.column_names(), cfg.warmup, diag_np.split_ess)
+    assert not fails, fails
+    # well-mixed: split R-hat on every parameter column
+    post = o["draws"][:, cfg.warmup:, 7:-1]
+    rh = [diag_np.split_rhat(post[:, :, j]) for j in range(post.shape[2])]
+    assert max(rh) < 1.01
+
+
+def _small(family="normal", N=48, Nn=5):
+    from fitoct_amd.synth import default_prior, synth_decay
+    t0, S0 = default_prior()
+    d = synth_decay(N, "sincExp", 3)
+    return ExpGPProblem(d["x"], d["y"], d["uy"], Nn=Nn, gridType="extremal", theta0=t0,
+                        Sigma0=S0, prior_type=family)
+
+
+def test_chain_addressing_is_shard_invariant():
+    """Chains are keyed by (seed, chain_offset + local id): running [0,6) in one
+    call equals [0,2) + [2,6) in two calls (what distributed sharding relies on)."""
+    prob = _small()
+    base = dict(warmup=40, samples=30, seed=11, max_treedepth=6)
+    full = nuts_c.sample(prob, SamplerConfig(chains=6, **base), nthreads=3)["draws"]
+    a = nuts_c.sample(prob, SamplerConfig(chains=2, **base), nthreads=2)["draws"]
+    b = nuts_c.sample(prob, SamplerConfig(chains=4, chain_offset=2, **base), nthreads=2)["draws"]
+    np.testing.assert_array_equal(np.concatenate([a, b]), full)
+
+
+def test_deterministic_and_seed_sensitive():
+    prob = _small("lasso")
+    cfg = SamplerConfig(chains=3, warmup=30, samples=20, seed=5, max_treedepth=6)
+    d1 = nuts_c.sample(prob, cfg, nthreads=3)["draws"]
+    d2 = nuts_c.sample(prob, cfg, nthreads=1)["draws"]
+    np.testing.assert_array_equal(d1, d2)
+    cfg.seed = 6
+    assert not np.array_equal(d1, nuts_c.sample(prob, cfg, nthreads=3)["draws"])
+
+
+@pytest.mark.parametrize("path", golden_files("draws"), ids=lambda p: os.path.basename(p))
+def test_oracle_reproduces_draw_fixture(path):
+    fx = load_golden(path)
+    m = fx["meta"]
+    prob = ExpGPProblem(fx["x"], fx["y"], fx["uy"], Nn=m["Nn"], gridType=m["grid_type"],
+                        theta0=fx["theta0"], Sigma0=fx["Sigma0"], prior_type=m["family"])
+    cfg = SamplerConfig(chains=m["chains"], warmup=m["warmup"], samples=m["samples"],
+                        seed=m["seed"], max_treedepth=m["max_treedepth"])
+    o = nuts_c.sample(prob, cfg, nthreads=4)
+    np.testing.assert_allclose(o["draws"], fx["draws"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_array_equal(o["leapfrogs"], fx["leapfrogs"])
+
+
+def test_sampler_columns_consistent():
+    """Stan sampler diagnostics columns: treedepth/n_leapfrog relation, accept in
+    [0,1], stepsize constant after warmup, sigma/theta positive, br >= 0."""
+    prob = _small("horseshoe", Nn=4)
+    cfg = SamplerConfig(chains=2, warmup=60, samples=40, seed=3, max_treedepth=6)
+    d = nuts_c.sample(prob, cfg, nthreads=2)["draws"]
+    cols = prob.column_names()
+    c = {n: i for i, n in enumerate(cols)}
+    td, nl = d[..., c["treedepth__"]], d[..., c["n_leapfrog__"]]
+    # base_nuts: depth_ is not incremented when the subtree just built is invalid
+    assert np.all(nl >= 2 ** td - 1) and np.all(nl <= 2 ** (td + 1) - 1)
+    acc = d[..., c["accept_stat__"]]
+    assert np.all((acc >= 0) & (acc <= 1))
+    eps = d[:, cfg.warmup:, c["stepsize__"]]
+    assert np.all(eps == eps[:, :1])
+    assert np.all(d[..., c["sigma"]] > 0) and np.all(d[..., c["theta.3"]] > 0)
+    assert np.all(d[..., c["br"]] >= 0)
+    assert np.all(td <= cfg.max_treedepth)
