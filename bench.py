@@ -1,0 +1,248 @@
+"""Headline benchmark: posterior draws/sec of FitOCT's ExpGP posterior on MI355X.
+
+Workload (BASELINE.json configs[2]): ``fitExpGP`` + horseshoe prior
+(Tests/horseShoePrior.stan, nu = 1), N = 2048 depth bins, Nn = 15 extremal control
+points (ctrlParams.yaml:3-5), 1024 chains per GPU, 500 warmup + 1000 sampling
+iterations per chain (FitOCT.R:43-44), adapt_delta 0.8, max_treedepth 10, all
+draws (warmup included, save_warmup) written to HBM.  Synthetic data: the
+restated synthData.R decay (fitoct_amd/synth.py, 'sincExp').
+
+A *step* = one complete sampler run of the local chains (plan launch: init,
+step-size search, adaptation, sampling); for N > 1 ranks it also includes the
+single RCCL gather of every rank's draws to rank 0.  Inputs are staged in HBM
+(plan creation) before the timed region.  Each step uses a fresh seed.
+
+    value = n_gpus * chains * samples / (max over ranks of wall per step)
+
+Extra objects on the JSON line: ``roofline`` (FP64 vector roofline of the
+sampler kernel: algorithmic flop F_grad = 4*N*Nn + 20*N per gradient, SURVEY.md
+§8d, x leapfrogs counted by the kernel / kernel time from HIP events on the
+launch stream; HBM traffic from the committed rocprofv3 PMC summary) and
+``cpu_baseline`` (the C oracle NUTS on this host's cores, bounded sample, scaled
+to the same unit -- see DESIGN.md §Measurement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_BINS, NN, CHAINS, WARMUP_IT, SAMPLES = 2048, 15, 1024, 500, 1000
+FP64_VALU_PEAK_TF = 78.6          # MI355X FP64 vector peak (vendor spec; 1/2 of FP32 vector)
+HBM_PEAK_GBS = 8000.0
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def f_grad(N, Nn):
+    return 4 * N * Nn + 20 * N     # SURVEY.md §8d algorithmic flop per gradient
+
+
+def make_problem():
+    from fitoct_amd import ExpGPProblem
+    from fitoct_amd.synth import default_prior, synth_decay
+    t0, S0 = default_prior()
+    d = synth_decay(N_BINS, "sincExp", 1234)
+    return ExpGPProblem(d["x"], d["y"], d["uy"], dataType=2, Nn=NN, gridType="extremal",
+                        theta0=t0, Sigma0=S0, prior_type="horseshoe", nu=1.0)
+
+
+def make_config(seed, chains, offset, device, warmup_it, samples):
+    from fitoct_amd import SamplerConfig
+    return SamplerConfig(chains=chains, chain_offset=offset, warmup=warmup_it, samples=samples,
+                         seed=seed, adapt_delta=0.8, max_treedepth=10, device=device)
+
+
+def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, seconds_target=20.0):
+    """C oracle (oracle/fitoct_oracle.c, OpenMP over chains) on ``threads`` host
+    cores: a bounded run of the same problem (one chain per thread, 150 warmup +
+    100 draws), its leapfrog rate scaled by the GPU step's leapfrogs per draw."""
+    from oracle import nuts_c
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = max(1, min(16, avail))
+    W, S = 150, 100
+    cfg = make_config(7, threads, 900_000, 0, W, S)
+    t = time.perf_counter()
+    o = nuts_c.sample(prob, cfg, nthreads=threads)
+    wall = time.perf_counter() - t
+    lf = int(o["leapfrogs"].sum())
+    lf_rate = lf / wall
+    value = draws_per_step * lf_rate / gpu_lf_per_step
+    return {"value": value, "unit": "draws/s", "cores": threads, "kind": "port",
+            "sample": (f"C oracle NUTS, {threads} chains x ({W} warmup + {S} draws) of the same "
+                       f"problem on {threads} threads: {lf} gradients in {wall:.1f} s "
+                       f"({lf_rate:.3g} grad/s); scaled by the GPU step's "
+                       f"{gpu_lf_per_step / draws_per_step:.1f} gradients per post-warmup draw"),
+            "wall_s": round(wall, 2)}
+
+
+def load_traffic(workload):
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+        if t.get("workload") == workload:
+            return t
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--chains", type=int, default=CHAINS, help="chains per GPU")
+    ap.add_argument("--iters", type=str, default=f"{WARMUP_IT},{SAMPLES}",
+                    help="sampler warmup,samples per chain")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--precision", default="f64", choices=["f64", "mixed"])
+    args = ap.parse_args()
+    W_it, S_it = (int(v) for v in args.iters.split(","))
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from fitoct_amd import Plan
+    from fitoct_amd.api import SamplerConfig  # noqa: F401  (import check)
+    from fitoct_amd.stanfit import split_rhat_ess
+
+    prob = make_problem()
+    C = args.chains
+    offset = rank * C
+
+    def plan_for(step):
+        cfg = make_config(1000 + step, C, offset, local, W_it, S_it)
+        cfg.precision = args.precision
+        return Plan(prob, cfg)
+
+    stream = torch.cuda.current_stream(dev)
+    info = None
+    bufs = {}
+
+    def run_step(pl):
+        nonlocal info
+        info = pl.info
+        key = info["draws_bytes"]
+        if key not in bufs:
+            bufs[key] = torch.empty(key // 8, dtype=torch.float64, device=dev)
+            if world > 1 and rank == 0:
+                bufs["gather"] = [torch.empty_like(bufs[key]) for _ in range(world)]
+        buf = bufs[key]
+        pl.run(d_draws=buf.data_ptr(), stream=stream.cuda_stream)
+        if world > 1:
+            dist.gather(buf, gather_list=bufs.get("gather") if rank == 0 else None, dst=0)
+        return buf
+
+    # ---- untimed warmup steps -------------------------------------------------
+    for w in range(args.warmup):
+        with plan_for(-1 - w) as pl:
+            run_step(pl)
+    torch.cuda.synchronize()
+
+    plans = [plan_for(s) for s in range(args.steps)]     # inputs staged in HBM up front
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    for pl in plans:
+        run_step(pl)
+        kernel_ms.append(pl.download(with_draws=False).kernel_ms)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    outs = [pl.download(with_draws=(i == len(plans) - 1)) for i, pl in enumerate(plans)]
+    lf_steps = [o.total_leapfrogs for o in outs]
+    if dist is not None:
+        t = torch.tensor(lf_steps, dtype=torch.float64, device=dev)
+        dist.all_reduce(t)
+        lf_all = t.cpu().numpy()
+    else:
+        lf_all = np.array(lf_steps, dtype=np.float64)
+
+    ms_per_step = wall * 1e3 / args.steps
+    draws_step = world * C * S_it
+    value = draws_step / (ms_per_step / 1e3)
+
+    # convergence of the last step (rank 0's chains): split R-hat over parameters
+    last = outs[-1].draws
+    cols = prob.column_names()
+    W_saved = outs[-1].warmup_saved
+    rh = [split_rhat_ess(last[:, W_saved:, j])[0] for j, n in enumerate(cols)
+          if j >= 7 and not n.startswith("r2_")]
+    divergent = float(last[:, W_saved:, 5].mean())
+    lf_per_draw = float(np.mean(lf_steps)) / (C * (W_it + S_it))
+
+    workload = (f"fitExpGP+horseshoe N={N_BINS} Nn={NN} {C} chains/GPU "
+                f"W={W_it} S={S_it} treedepth<=10")
+    kms = float(np.mean(kernel_ms))
+    flops = f_grad(N_BINS, NN) * float(np.mean(lf_steps))
+    achieved = flops / (kms / 1e3) / 1e12
+    traffic = load_traffic(workload)
+    roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TF,
+            "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TF, 4),
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "kernel": "nuts_kernel", "kernel_ms": round(kms, 2),
+            "flop_per_gradient": f_grad(N_BINS, NN),
+            "gradients_per_launch": int(np.mean(lf_steps))}
+    if traffic:
+        roof["hbm_gbs"] = round(traffic["bytes_per_launch"] / (kms / 1e3) / 1e9, 2)
+        roof["hbm_frac"] = round(roof["hbm_gbs"] / HBM_PEAK_GBS, 5)
+        roof["traffic_source"] = os.path.relpath(TRAFFIC_FILE, ROOT)
+
+    line = {
+        "metric": "posterior draws/sec (all chains), ExpGP N=2048 @ 1024 chains; R-hat",
+        "value": round(value, 2), "unit": "draws/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64" if args.precision == "f64"
+        else "f32-sweep/f64-state", "data": "synthetic (restated synthData.R sincExp decay)",
+        "config": {"workload": workload, "prior": "horseshoe", "N": N_BINS, "Nn": NN,
+                   "chains_per_gpu": C, "global_chains": world * C, "warmup_iters": W_it,
+                   "samples": S_it, "adapt_delta": 0.8, "max_treedepth": 10,
+                   "parallelism": f"chains sharded over {world} GPU(s)"},
+        "rhat_max": round(max(rh), 5), "divergent_frac": round(divergent, 5),
+        "gradients_per_iteration": round(lf_per_draw, 1),
+        "total_gradients_per_step": float(lf_all.mean()),
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(prob, float(np.mean(lf_steps)), C * S_it)
+    for pl in plans:
+        pl.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -105,6 +105,21 @@ class FitOCTError(RuntimeError):
         self.code = code
 
 
+def _single_hip_runtime():
+    """Keep ONE HIP runtime per process.  PyTorch-ROCm bundles its own
+    libamdhip64 (soname libamdhip64.so.7, the same as /opt/rocm's); if libfitoct
+    loaded /opt/rocm's copy first, torch would later load a second HIP/HSA
+    runtime and find no GPU.  Loading torch first makes the dynamic linker bind
+    libfitoct to torch's already-loaded runtime.  Without torch (e.g. the R
+    shim) libfitoct uses /opt/rocm's runtime."""
+    if os.environ.get("FITOCT_SYSTEM_HIP_RUNTIME"):
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib():
     """Load the in-tree libfitoct.so (fails loudly if it was not built)."""
     global _LIB
@@ -113,6 +128,7 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} not found: build it with `python -m fitoct_amd.build` "
                 "(the HIP sampler has no CPU fallback)")
+        _single_hip_runtime()
         L = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             f = getattr(L, name)
