@@ -59,17 +59,17 @@ def make_config(seed, chains, offset, device, warmup_it, samples):
                          seed=seed, adapt_delta=0.8, max_treedepth=10, device=device)
 
 
-def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, seconds_target=20.0):
+def cpu_baseline(prob, gpu_lf_per_step, draws_per_step):
     """C oracle (oracle/fitoct_oracle.c, OpenMP over chains) on ``threads`` host
-    cores: a bounded run of the same problem (one chain per thread, 150 warmup +
-    100 draws), its leapfrog rate scaled by the GPU step's leapfrogs per draw."""
+    cores: a bounded run of the same problem (one chain per thread, 250 warmup +
+    250 draws, ~10-20 s), its leapfrog rate scaled by the GPU step's leapfrogs per draw."""
     from oracle import nuts_c
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
     threads = max(1, min(16, avail))
-    W, S = 150, 100
+    W, S = 250, 250
     cfg = make_config(7, threads, 900_000, 0, W, S)
     t = time.perf_counter()
     o = nuts_c.sample(prob, cfg, nthreads=threads)
