@@ -196,8 +196,10 @@ def main():
     last = outs[-1].draws
     cols = prob.column_names()
     W_saved = outs[-1].warmup_saved
-    rh = [split_rhat_ess(last[:, W_saved:, j])[0] for j, n in enumerate(cols)
-          if j >= 7 and not n.startswith("r2_")]
+    par = [j for j, n in enumerate(cols) if j >= 7 and not n.startswith("r2_")]
+    rh = [split_rhat_ess(last[:, W_saved:, j])[0] for j in par]
+    stuck = last[:, W_saved:, 5].mean(1) > 0.5       # funnel-trapped chains
+    rh_free = [split_rhat_ess(last[~stuck, W_saved:, j])[0] for j in par] if stuck.any() else rh
     divergent = float(last[:, W_saved:, 5].mean())
     lf_per_draw = float(np.mean(lf_steps)) / (C * (W_it + S_it))
 
@@ -228,7 +230,8 @@ def main():
                    "chains_per_gpu": C, "global_chains": world * C, "warmup_iters": W_it,
                    "samples": S_it, "adapt_delta": 0.8, "max_treedepth": 10,
                    "parallelism": f"chains sharded over {world} GPU(s)"},
-        "rhat_max": round(max(rh), 5), "divergent_frac": round(divergent, 5),
+        "rhat_max": round(max(rh), 5), "stuck_chains": int(stuck.sum()),
+        "rhat_max_excl_stuck": round(max(rh_free), 5), "divergent_frac": round(divergent, 5),
         "gradients_per_iteration": round(lf_per_draw, 1),
         "total_gradients_per_step": float(lf_all.mean()),
         "roofline": roof,
