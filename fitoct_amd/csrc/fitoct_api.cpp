@@ -543,8 +543,8 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
   long long* d_stamps = nullptr;
   const bool want_stamps = getenv("FITOCT_STAMPS") != nullptr;   // diagnostic only
   if (want_stamps) {
-    HIP_TRY(hipMalloc(&d_stamps, sizeof(long long) * 40 * pl->tiles));
-    HIP_TRY(hipMemsetAsync(d_stamps, 0, sizeof(long long) * 40 * pl->tiles, st));
+    HIP_TRY(hipMalloc(&d_stamps, sizeof(long long) * NSTAMP * pl->tiles));
+    HIP_TRY(hipMemsetAsync(d_stamps, 0, sizeof(long long) * NSTAMP * pl->tiles, st));
     k.stamps = d_stamps;
   }
   HIP_TRY(hipEventRecord(pl->ev0, st));
@@ -558,22 +558,32 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
   pl->kernel_ms = ms;
   pl->last_draws = dst;
   if (want_stamps) {
-    std::vector<long long> h((size_t)40 * pl->tiles);
+    std::vector<long long> h((size_t)NSTAMP * pl->tiles);
     HIP_TRY(hipMemcpy(h.data(), d_stamps, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
     (void)hipFree(d_stamps);
-    double steps = 0, tg = 0, tn = 0, tt = 0, smax = 0;
+    double steps = 0, tg = 0, tn = 0, tt = 0, smax = 0, tw = 0, nw = 0;
     double act_t[18] = {0}, act_n[18] = {0};
     for (int t = 0; t < pl->tiles; ++t) {
-      steps += h[40 * t];
-      tg += h[40 * t + 1];
-      tn += h[40 * t + 2];
-      tt += h[40 * t + 3];
-      smax = std::max(smax, (double)h[40 * t]);
+      const long long* o = h.data() + (size_t)NSTAMP * t;
+      steps += o[0];
+      tg += o[1];
+      tn += o[2];
+      tt += o[3];
+      tw += o[40];
+      nw += o[41];
+      smax = std::max(smax, (double)o[0]);
       for (int a = 0; a < 18; ++a) {
-        act_t[a] += h[40 * t + 4 + a];
-        act_n[a] += h[40 * t + 22 + a];
+        act_t[a] += o[4 + a];
+        act_n[a] += o[22 + a];
       }
     }
+    double subt[12] = {0};
+    for (int t = 0; t < pl->tiles; ++t)
+      for (int k = 0; k < 12; ++k) subt[k] += h[(size_t)NSTAMP * t + 48 + k];
+    fprintf(stderr, "[fitoct stamps] sub-action cycles per leaf (chain 0): ");
+    for (int k = 0; k < 12; ++k)
+      if (subt[k] > 0) fprintf(stderr, "s%d:%.0f ", k, subt[k] / std::max(act_n[11], 1.0));
+    fprintf(stderr, "\n");
     fprintf(stderr, "[fitoct stamps] per action (chain 0 of each tile): ");
     for (int a = 1; a < 18; ++a)
       if (act_n[a] > 0) fprintf(stderr, "a%d:%.0fx%.0f ", a, act_n[a] / pl->tiles, act_t[a] / act_n[a]);
@@ -582,6 +592,8 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
             "[fitoct stamps] tiles=%d mean sweeps/tile=%.0f max=%.0f | per sweep: grad-wave busy %.0f "
             "nuts-wave busy %.0f wall %.0f memtime ticks\n",
             pl->tiles, steps / pl->tiles, smax, tg / steps, tn / steps, tt / steps);
+    fprintf(stderr, "[fitoct stamps] chain 0 per NUTS round: busy %.0f, waiting for its gradient %.0f\n",
+            tn / std::max(nw, 1.0), tw / std::max(nw, 1.0));
   }
   pl->ran = true;
   return FITOCT_OK;

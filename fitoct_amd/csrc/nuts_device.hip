@@ -52,6 +52,14 @@
 
 namespace fitoct {
 
+// Explicit address spaces: LDS (3), global (1), constant (4).  Generic pointers
+// would compile to FLAT instructions, which count in both vmcnt and lgkmcnt --
+// every LDS wait would then also wait for the sampler's outstanding HBM stores.
+#define AS_LDS __attribute__((address_space(3)))
+#define AS_GLB __attribute__((address_space(1)))
+#define AS_CST __attribute__((address_space(4)))
+using KPc = const AS_CST KParams;
+
 enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2 };
 enum { ERR_INIT = -4, ERR_NUMERIC = -5, ERR_TIMEOUT = -6 };
 
@@ -64,23 +72,27 @@ enum VecId : int {
   V_MINV, V_WF_M, V_WF_M2,     // metric + Welford
   V_RHO, V_PNEAR,              // trajectory momentum sum, near end of old trajectory
   V_QS, V_QE,                  // staged q and its constrained values (exp on positive params)
+  V_PG, V_CA,                  // prior part of grad, likelihood coefficient (prior_part)
   NVEC
 };
 // U-turn record of one tree level (LDS)
 enum LvlId : int { K_PBEG = 0, K_PEND = 1, K_RHO = 2, NLVL = 3 };
 // proposal pool slot (HBM)
 enum PoolId : int { P_Q = 0, P_P = 1, P_G = 2, NPOOL = 3 };
-constexpr int NAUX = 64;   // per chain: yGP[32] | horseshoe lambda_j*tau [32]
+constexpr int NAUX = 96;   // per chain: yGP[32] | horseshoe lambda_j*tau [32] | FW_j [32]
 
 struct ChainScalars {
   int state, t, depth, leaf, dir, n_leapfrog, divergent, init_attempt;
   int da_counter, win_counter, win_size, win_next, wf_n, ss_trial, ss_dir, ss_window;
-  int status, win_on, init_buf, term_buf, pool_used, pad0, pad1, pad2;
+  int status, win_on, init_buf, term_buf, pool_used, lsw_e, pad1, pad2;
   int st_prop[MAXDEPTH];
-  double H0, lsw, sum_metro, eps, eps_used, mu, s_bar, x_bar, ss_H0, lf_e;
+  int st_w_e[MAXDEPTH];
+  double H0, lsw_m, sum_metro, eps, eps_used, mu, s_bar, x_bar, ss_H0, lf_e;
   double cur_lp, cur_s2, smp_lp, smp_s2;
+  double pr_lp, pr_is2, u_top, pad4;
+  double u_merge[MAXDEPTH];
   double end_lp[2], end_s2[2];
-  double st_lsw[MAXDEPTH];
+  double st_w_m[MAXDEPTH];
   double pool_lp[MAXDEPTH + 1], pool_s2[MAXDEPTH + 1];
   long long leapfrogs;
   long long pad3;
@@ -109,6 +121,13 @@ __device__ __forceinline__ double dpp(double x) {
   const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
   return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// v_readlane of a double (lane index wave-uniform)
+__device__ __forceinline__ double rl(double x, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 // a' = a with rows {1,3} (lanes 16-31, 48-63) replaced by b's rows {0,2};
 // b' = b with rows {0,2} replaced by a's rows {1,3}.  Returns a' + b'.
@@ -154,13 +173,61 @@ __device__ __forceinline__ void wave_sum2(double& a, double& b) {
   b = swap32_add(b, b);
 }
 
-__device__ __forceinline__ double lse(double a, double b) {
-  // log_sum_exp with -inf handling (stan::math::log_sum_exp)
-  if (a == -INFINITY) return b;
-  if (b == -INFINITY) return a;
-  const double m = a > b ? a : b;
-  return m + log1p(exp(-fabs(a - b)));
+// N independent butterfly sums, stage by stage (the DPP / permlane moves of the
+// N values overlap instead of serialising N reductions)
+template <int N>
+__device__ __forceinline__ void wave_sum_n(double (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] += dpp<DPP_XOR1>(x[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] += dpp<DPP_XOR2>(x[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] += dpp<DPP_HALF_MIRROR>(x[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] += dpp<DPP_MIRROR>(x[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] = swap16_add(x[i], x[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) x[i] = swap32_add(x[i], x[i]);
 }
+
+// Multinomial trajectory weights exp(H0 - H) as extended-exponent floats
+// m * 2^e (m in [1/2, 1) or 0): the merges of base_nuts (log_sum_exp of log
+// weights, then u < exp(lsw_final - lsw_subtree)) become an add and a multiply,
+// with no exp / log1p per merge and no overflow for any energy change.  The
+// oracle (oracle/fitoct_oracle.c) uses the same representation.
+struct XF {
+  double m;
+  int e;
+};
+__device__ __forceinline__ XF xf_norm(double m, int e) {
+  int k;
+  const double f = frexp(m, &k);
+  return XF{f, f == 0.0 ? 0 : e + k};
+}
+__device__ __forceinline__ XF xf_exp(double x) {   // exp(x), x <= +inf; -inf -> 0
+  if (x > -700.0 && x < 700.0) return xf_norm(exp(x), 0);
+  if (!(x > -INFINITY)) return XF{0.0, 0};
+  const double k = floor(x * 1.4426950408889634);   // log2(e)
+  return xf_norm(exp(fma(-k, 0.6931471805599453, x)), (int)k);
+}
+__device__ __forceinline__ XF xf_add(XF a, XF b) {
+  if (a.m == 0.0) return b;
+  if (b.m == 0.0) return a;
+  const int e = a.e > b.e ? a.e : b.e;
+  return xf_norm(ldexp(a.m, a.e - e) + ldexp(b.m, b.e - e), e);
+}
+__device__ __forceinline__ bool xf_gt(XF a, XF b) {   // a > b (both >= 0)
+  if (a.m == 0.0) return false;
+  if (b.m == 0.0) return true;
+  return a.e != b.e ? a.e > b.e : a.m > b.m;
+}
+__device__ __forceinline__ bool xf_u_below(double u, XF a, XF b) {   // u < a / b
+  if (b.m == 0.0) return false;   // Stan: u < exp(-inf - -inf) = NaN is false
+  return ldexp(u * b.m, b.e - a.e) < a.m;
+}
+__device__ __forceinline__ double xf_val(XF a) { return ldexp(a.m, a.e); }
+
 
 __device__ __forceinline__ void normal_pair(RngKey k, uint32_t c0, uint32_t c1, uint32_t c2,
                                             uint32_t c3, double& n0, double& n1) {
@@ -249,8 +316,8 @@ __device__ __forceinline__ void bin_rows(R cx, R y, R isu, const R (&Brow)[NNP],
 // step bit is set keep the upper half.  Bits 5 and 4 use the gfx950 permlane
 // swaps (no select needed), bits 3..1 DPP row mirrors (partner differs in the
 // step bit and below), the final pair a quad swap.
-template <int H, int CTRL>
-__device__ __forceinline__ void tr_dpp(double (&v)[NSLOT], bool up) {
+template <int H, int CTRL, int NV>
+__device__ __forceinline__ void tr_dpp(double (&v)[NV], bool up) {
 #pragma unroll
   for (int i = 0; i < H; ++i) {
     const double send = up ? v[i] : v[i + H];
@@ -258,6 +325,23 @@ __device__ __forceinline__ void tr_dpp(double (&v)[NSLOT], bool up) {
     v[i] = keep + dpp<CTRL>(send);
   }
 }
+// The same transposed butterfly for 8 values (U-turn criteria): after it every
+// lane of each 8-lane group holds the full sum of one value; returns whether all
+// 8 sums are > 0 (one ballot).  ~3x fewer cross-lane steps than 8 butterflies.
+__device__ __forceinline__ bool transpose_all_positive8(double (&v)[8], int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = swap32_add(v[i], v[i + 4]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) v[i] = swap16_add(v[i], v[i + 2]);
+  tr_dpp<1, DPP_MIRROR>(v, (lane & 8) != 0);
+  double x = v[0];
+  x += dpp<DPP_XOR1>(x);
+  x += dpp<DPP_XOR2>(x);
+  x += dpp<DPP_HALF_MIRROR>(x);
+  const uint64_t ok = __builtin_amdgcn_ballot_w64(x > 0.0);
+  return ok == __builtin_amdgcn_read_exec();
+}
+
 __device__ __forceinline__ double transpose_reduce32(double (&v)[NSLOT], int lane) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) v[i] = swap32_add(v[i], v[i + 16]);   // lanes >= 32 keep [16,32)
@@ -276,12 +360,12 @@ struct Bins {
   static constexpr int NR = MODE == MODE_POLY ? 2 : NNP;
   R cx[NB], y[NB], isu[NB];
   R row[NB][NR];
-  __device__ void load(const KParams& P, int tid) {
+  __device__ void load(KPc& P, int tid) {
     if constexpr (BPT > 0) {
-      const R* pcx = (const R*)P.cx;
-      const R* py = (const R*)P.y;
-      const R* pisu = (const R*)P.isu;
-      const R* pB = (const R*)P.B;
+      const AS_GLB R* pcx = (const AS_GLB R*)P.cx;
+      const AS_GLB R* py = (const AS_GLB R*)P.y;
+      const AS_GLB R* pisu = (const AS_GLB R*)P.isu;
+      const AS_GLB R* pB = (const AS_GLB R*)P.B;
 #pragma unroll
       for (int b = 0; b < BPT; ++b) {
         const int i = tid + b * GT;
@@ -311,29 +395,32 @@ struct Lds {
   static __host__ __device__ constexpr int bytes(int G, int max_depth) {
     return head_bytes(G) + G * chain_bytes(max_depth);
   }
-  char* base;
+  AS_LDS char* base;
   int G, cb;
-  __device__ double* kinv() const { return (double*)base; }
-  __device__ double* bv() const { return (double*)base + KMAX * KMAX; }
-  __device__ double* mp(int c) const { return (double*)(base + KBYTES) + c * MPW; }
-  __device__ double* part() const { return (double*)(base + KBYTES) + GMAX * MPW; }
-  __device__ char* chain(int c) const { return base + head_bytes(G) + c * cb; }
-  __device__ ChainScalars& cs(int c) const { return *(ChainScalars*)chain(c); }
-  __device__ double* vecs(int c) const { return (double*)(chain(c) + sizeof(ChainScalars)); }
-  __device__ double* sums(int c) const { return vecs(c) + NVEC * VLEN; }
-  __device__ double* aux(int c) const { return sums(c) + NSLOT; }
-  __device__ double* lvls(int c) const { return aux(c) + NAUX; }
+  __device__ AS_LDS double* kinv() const { return (AS_LDS double*)base; }
+  __device__ AS_LDS double* bv() const { return (AS_LDS double*)base + KMAX * KMAX; }
+  __device__ AS_LDS double* mp(int c) const { return (AS_LDS double*)(base + KBYTES) + c * MPW; }
+  __device__ AS_LDS double* part() const { return (AS_LDS double*)(base + KBYTES) + GMAX * MPW; }
+  __device__ AS_LDS char* chain(int c) const { return base + head_bytes(G) + c * cb; }
+  __device__ AS_LDS ChainScalars& cs(int c) const { return *(AS_LDS ChainScalars*)chain(c); }
+  __device__ AS_LDS double* vecs(int c) const {
+    return (AS_LDS double*)(chain(c) + sizeof(ChainScalars));
+  }
+  __device__ AS_LDS double* sums(int c) const { return vecs(c) + NVEC * VLEN; }
+  __device__ AS_LDS double* aux(int c) const { return sums(c) + NSLOT; }
+  __device__ AS_LDS double* lvls(int c) const { return aux(c) + NAUX; }
 };
 
 // The likelihood sweep of chains [cb, ce) of the tile (gradient waves only).
 // PART[wave][c][0 .. 4+NNP) receives this wave's partial sums of chain c.
 template <class R, int BPT, int NNP, int MODE>
-__device__ void gradient_pass(const KParams& P, const Bins<R, BPT, NNP, MODE>& bins,
-                              const double* mpall, double* part, const int* done, int cb, int ce,
+__device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
+                              const AS_LDS double* mpall, AS_LDS double* part, const int* done,
+                              int cb, int ce,
                               int tid, int lane, int wave) {
   for (int c = cb; c < ce; ++c) {
     if (done[c]) continue;   // wave-uniform (LDS broadcast)
-    const double* mp = mpall + c * MPW;
+    const AS_LDS double* mp = mpall + c * MPW;
     const R th1 = (R)mp[0], th2 = (R)mp[1], th3 = (R)mp[2];
     R cf[NNP];   // POLY: c_l = b_l (K^-1 yGP)_l ; ROWS: yGP_k
 #pragma unroll
@@ -358,10 +445,10 @@ __device__ void gradient_pass(const KParams& P, const Bins<R, BPT, NNP, MODE>& b
 #pragma unroll
       for (int k = 0; k < 4 + NNP; ++k) acc[k] = (double)racc[k];
     } else {
-      const R* pcx = (const R*)P.cx;
-      const R* py = (const R*)P.y;
-      const R* pisu = (const R*)P.isu;
-      const R* pB = (const R*)P.B;
+      const AS_GLB R* pcx = (const AS_GLB R*)P.cx;
+      const AS_GLB R* py = (const AS_GLB R*)P.y;
+      const AS_GLB R* pisu = (const AS_GLB R*)P.isu;
+      const AS_GLB R* pB = (const AS_GLB R*)P.B;
       for (int i = tid; i < P.n_pad; i += GT) {
         if constexpr (MODE == MODE_POLY) {
           bin_poly<R, NNP, double>(pcx[i], py[i], pisu[i], pB[2 * (size_t)i], pB[2 * (size_t)i + 1],
@@ -392,35 +479,33 @@ template <int PPL, int NNP>
 struct Chain {
   using V = Vd<PPL>;
   static constexpr int VLEN = WAVE * PPL;
-  const KParams* pp;   // laundered once per action: no kernarg load is hoisted across actions
-  ChainScalars* Sp;
-  double* Vb;
-  double* SUMS;
-  double* AUX;   // [0,32): yGP ; [32,64): horseshoe lambda_j * tau
-  double* LV;    // [max_depth][NLVL][VLEN]
-  double* MP;
-  double* part;
-  double* pool;  // HBM [max_depth+1][NPOOL][VLEN]
-  const double* Kinv;
-  const double* bv;
+  KPc* pp;   // laundered once per action: no kernarg load is hoisted across actions
+  AS_LDS ChainScalars* Sp;
+  AS_LDS double* Vb;
+  AS_LDS double* SUMS;
+  AS_LDS double* AUX;   // [0,32): yGP ; [32,64): horseshoe lambda_j * tau
+  AS_LDS double* LV;    // [max_depth][NLVL][VLEN]
+  AS_LDS double* MP;
+  AS_LDS double* part;
+  const AS_LDS double* Kinv;
+  const AS_LDS double* bv;
   int lane, slot, lc, gid, nct;
   RngKey key;
 
-  __device__ Chain(const KParams& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
+  __device__ Chain(KPc& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
       : pp(&P_), Sp(&L.cs(slot_)), Vb(L.vecs(slot_)), SUMS(L.sums(slot_)), AUX(L.aux(slot_)),
         LV(L.lvls(slot_)), MP(L.mp(slot_)), part(L.part()), Kinv(L.kinv()), bv(L.bv()),
         lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
     gid = Pr().chain_offset + lc;
     key = make_key(Pr().seed, (uint32_t)gid);
-    pool = Pr().stack ? Pr().stack + (size_t)lc * (Pr().max_depth + 1) * NPOOL * VLEN : nullptr;
   }
 
-  __device__ __forceinline__ const KParams& Pr() const { return *pp; }
+  __device__ __forceinline__ KPc& Pr() const { return *pp; }
   __device__ __forceinline__ int idx(int s) const { return s * WAVE + lane; }
   __device__ __forceinline__ bool ok(int s) const { return idx(s) < Pr().D; }
-  __device__ __forceinline__ double* vec(int v) const { return Vb + v * VLEN; }
-  __device__ __forceinline__ const double* QS() const { return Vb + V_QS * VLEN; }
-  __device__ __forceinline__ const double* QE() const { return Vb + V_QE * VLEN; }
+  __device__ __forceinline__ AS_LDS double* vec(int v) const { return Vb + v * VLEN; }
+  __device__ __forceinline__ const AS_LDS double* QS() const { return Vb + V_QS * VLEN; }
+  __device__ __forceinline__ const AS_LDS double* QE() const { return Vb + V_QE * VLEN; }
   __device__ __forceinline__ V ld(int v) const {
     V r;
 #pragma unroll
@@ -432,23 +517,26 @@ struct Chain {
     for (int s = 0; s < PPL; ++s) vec(v)[idx(s)] = x.a[s];
   }
   __device__ __forceinline__ void copyv(int dst, int src) const { st(dst, ld(src)); }
-  __device__ __forceinline__ double* lvl(int level, int which) const {
+  __device__ __forceinline__ AS_LDS double* lvl(int level, int which) const {
     return LV + ((size_t)level * NLVL + which) * VLEN;
   }
   __device__ __forceinline__ V lld(int level, int which) const {
     V r;
-    const double* p = lvl(level, which);
+    const AS_LDS double* p = lvl(level, which);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) r.a[s] = p[idx(s)];
     return r;
   }
   __device__ __forceinline__ void lst(int level, int which, const V& x) const {
-    double* p = lvl(level, which);
+    AS_LDS double* p = lvl(level, which);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) p[idx(s)] = x.a[s];
   }
-  __device__ __forceinline__ double* pslot(int sl, int which) const {
-    return pool + ((size_t)sl * NPOOL + which) * VLEN;
+  __device__ __forceinline__ AS_GLB double* pslot(int sl, int which) const {
+    // HBM [chain][max_depth+1][NPOOL][VLEN]; recomputed from the parameter block
+    // on use (scalar ops) instead of holding a 64-bit pointer across actions
+    const size_t base = ((size_t)lc * (Pr().max_depth + 1) + sl) * NPOOL + which;
+    return (AS_GLB double*)Pr().stack + base * VLEN;
   }
 
   __device__ __forceinline__ double kin(const V& p, const V& minv) const {
@@ -469,16 +557,35 @@ struct Chain {
     wave_sum2(x, y);
     return x > 0.0 && y > 0.0;
   }
+  // three compute_criterion calls of one merge, reduced together (6 dot products
+  // in one interleaved butterfly; the conjunction is order-independent)
+  __device__ __forceinline__ bool crit3(const V& a1, const V& b1, const V& r1, const V& a2,
+                                        const V& b2, const V& r2, const V& a3, const V& b3,
+                                        const V& r3, const V& minv) const {
+    // slots 6, 7 pad the transposed reduction with a positive constant (lane 0)
+    double x[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, lane == 0 ? 1.0 : 0.0, lane == 0 ? 1.0 : 0.0};
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) {
+      x[0] += minv.a[s] * b1.a[s] * r1.a[s];
+      x[1] += minv.a[s] * a1.a[s] * r1.a[s];
+      x[2] += minv.a[s] * b2.a[s] * r2.a[s];
+      x[3] += minv.a[s] * a2.a[s] * r2.a[s];
+      x[4] += minv.a[s] * b3.a[s] * r3.a[s];
+      x[5] += minv.a[s] * a3.a[s] * r3.a[s];
+    }
+    return transpose_all_positive8(x, lane);
+  }
   __device__ __forceinline__ bool is_log(int k) const { return k < 3 || k >= 3 + Pr().Nn; }
 
   // ---------------- the point handed to the gradient phase ------------------
   // Stages q, caches its constrained values (QE) and, per family, yGP and the
   // horseshoe scales (AUX), then writes the gradient phase's parameters MP:
   // theta[3] and, per basis mode, yGP (rows) or c = b .* K^-1 yGP (poly).
+  // (LDS exchange: on gfx950 a v_readlane assembly of yGP measured 3x slower.)
   __device__ void write_mp(const V& q) const {
     const int Nn = Pr().Nn;
-    double* qs = vec(V_QS);
-    double* qe = vec(V_QE);
+    AS_LDS double* qs = vec(V_QS);
+    AS_LDS double* qe = vec(V_QE);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
@@ -540,94 +647,136 @@ struct Chain {
     wave_fence();
   }
 
-  __device__ double complete(V& g) const {
+  // The lp / grad completion is split so that everything depending only on the
+  // staged position runs while the gradient waves sweep the bins (prior_part,
+  // off the critical path), and only a few FMAs per lane remain once the bin
+  // sums arrive (lik_part):
+  //   grad_k = PG_k + CA_k * S[sidx(k)] + CB_k * famsum,   lp = pr_lp - 0.5 S0 pr_is2
+  // with S = SUMS after gather_sums and famsum = sum_j FW_j S[4+j] (horseshoe).
+  __device__ __forceinline__ int sidx(int k) const {   // which bin sum lane k's gradient needs
+    const int D = Pr().D, Nn = Pr().Nn;
+    if (k < 3) return 1 + k;
+    if (k == D - 1) return 0;
+    if (k < 3 + Nn) return 4 + (k - 3);
+    if (Pr().family == FAM_HORSESHOE && k >= 5 + Nn) return 4 + ((k - 5 - Nn) % Nn);
+    return 0;
+  }
+
+  __device__ void prior_part() const {
     const int D = Pr().D, Nn = Pr().Nn, fam = Pr().family;
-    const double* qs = QS();
-    const double* qe = QE();
+    const AS_LDS double* qs = QS();
+    const AS_LDS double* qe = QE();
     const bool lik = (Pr().prior_PD == 0);
-    const double Sd2 = SUMS[0];
-    const bool bad = lik && !(Sd2 <= DBL_MAX);
     const double th0 = qe[0], th1 = qe[1], th2 = qe[2];
     const double usig = qs[D - 1], sig = qe[D - 1], is2 = 1.0 / (sig * sig);
     const double d0 = th0 - Pr().theta0[0], d1 = th1 - Pr().theta0[1], d2 = th2 - Pr().theta0[2];
-    const double* Si = Pr().S0inv;
+    const AS_CST double* Si = Pr().S0inv;
     const double Sd0 = Si[0] * d0 + Si[1] * d1 + Si[2] * d2;
     const double Sd1 = Si[3] * d0 + Si[4] * d1 + Si[5] * d2;
     const double Sd2t = Si[6] * d0 + Si[7] * d1 + Si[8] * d2;
     const double ss = Pr().sigma_scale;
-    const double gyf = lik ? th1 * th2 * is2 : 0.0;   // dlp/dyGP_k = gyf * SUMS[4+k]
-    double lpc = 0.0, lpc2 = 0.0;
+    const double gyf = lik ? th1 * th2 * is2 : 0.0;   // dlp/dyGP_k = gyf * S[4+k]
+    double lpc = 0.0;
     if (lane == 0) {
-      if (lik) lpc += -0.5 * Sd2 * is2 - (double)Pr().N * usig;
+      if (lik) lpc += -(double)Pr().N * usig;
       lpc += -0.5 * (d0 * Sd0 + d1 * Sd1 + d2 * Sd2t) + qs[0] + qs[1] + qs[2];
       lpc += -0.5 * (sig / ss) * (sig / ss) + usig;
     }
-    // family-wide sums: normal sum yGP^2 ; horseshoe sum_j G_j yGP_j
-    if (lane < Nn) {
-      const double yv = AUX[lane];
-      lpc2 = (fam == FAM_HORSESHOE) ? gyf * SUMS[4 + lane] * yv : yv * yv;
-    }
-    double famsum = lpc2;
-    if (fam != FAM_LASSO) famsum = wave_sum(lpc2);
+    double ysum = 0.0;   // normal family: sum yGP^2
+    if (fam == FAM_NORMAL) ysum = wave_sum(lane < Nn ? AUX[lane] * AUX[lane] : 0.0);
+    if (fam == FAM_HORSESHOE && lane < Nn) AUX[64 + lane] = gyf * AUX[lane];   // FW_j
+    V pg, ca;
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
-      double gk = 0.0;
+      double gk = 0.0, ck = 0.0;
       if (k < D) {
         const double qk = qs[k];
         if (k < 3) {
-          double gl = 0.0;
-          if (lik) gl = (k == 0) ? SUMS[1] * is2 : (k == 1) ? SUMS[2] * is2 : th1 * SUMS[3] * is2 / th2;
           const double thk = (k == 0) ? th0 : (k == 1) ? th1 : th2;
           const double sdk = (k == 0) ? Sd0 : (k == 1) ? Sd1 : Sd2t;
-          gk = thk * (gl - sdk) + 1.0;
+          gk = 1.0 - thk * sdk;
+          if (lik) ck = (k == 2) ? th1 * is2 : thk * is2;
         } else if (k == D - 1) {
-          const double gl = lik ? (Sd2 * is2 - (double)Pr().N) / sig : 0.0;
-          gk = sig * (gl - sig / (ss * ss)) + 1.0;
+          gk = (lik ? -(double)Pr().N : 0.0) - sig * sig / (ss * ss) + 1.0;
+          if (lik) ck = is2;
         } else if (fam == FAM_NORMAL) {
           const double lam = qe[3 + Nn];
           if (k < 3 + Nn) {
-            gk = gyf * SUMS[4 + (k - 3)] - qk / (lam * lam);
+            gk = -qk / (lam * lam);
+            ck = gyf;
             lpc += -qk * qk / (2.0 * lam * lam);
           } else {  // lambda
             const double rate = Pr().lambda_rate_eff;
-            gk = lam * (-(double)Nn / lam + famsum / (lam * lam * lam) - rate) + 1.0;
+            gk = lam * (-(double)Nn / lam + ysum / (lam * lam * lam) - rate) + 1.0;
             lpc += -(double)Nn * qk - rate * lam + qk;
           }
         } else if (fam == FAM_LASSO) {
           const double ls = Pr().lambda_scale;
           const double sg = (qk > 0.0) ? 1.0 : (qk < 0.0) ? -1.0 : 0.0;
-          gk = gyf * SUMS[4 + (k - 3)] - ls * sg - 2.0 * ls * qk;
+          gk = -ls * sg - 2.0 * ls * qk;
+          ck = gyf;
           lpc += -ls * fabs(qk) - ls * qk * qk;
         } else {  // horseshoe (Tests/horseShoePrior.stan:25-43)
           const double nu = Pr().nu, ek = qe[k];
           if (k < 3 + Nn) {
-            const int j = k - 3;
-            gk = gyf * SUMS[4 + j] * AUX[32 + j] - qk;
+            gk = -qk;
+            ck = gyf * AUX[32 + (k - 3)];
             lpc += -0.5 * qk * qk;
           } else if (k == 3 + Nn) {
-            gk = famsum - ek * ek + 1.0;
+            gk = 1.0 - ek * ek;
             lpc += -0.5 * ek * ek + qk;
           } else if (k == 4 + Nn) {
-            gk = 0.5 * famsum - 1.5 + 0.5 / ek + 1.0;
+            gk = 0.5 / ek - 0.5;
             lpc += -1.5 * qk - 0.5 / ek + qk;
           } else if (k < 5 + 2 * Nn) {
-            const int j = k - 5 - Nn;
-            const double Gy = gyf * SUMS[4 + j] * AUX[j];
-            gk = Gy - ek * ek + 1.0;
+            gk = 1.0 - ek * ek;
+            ck = gyf * AUX[k - 5 - Nn];
             lpc += -0.5 * ek * ek + qk;
           } else {
-            const int j = k - 5 - 2 * Nn;
-            const double Gy = gyf * SUMS[4 + j] * AUX[j];
-            gk = 0.5 * Gy - (0.5 * nu + 1.0) + 0.5 * nu / ek + 1.0;
+            gk = -0.5 * nu + 0.5 * nu / ek;
+            ck = 0.5 * gyf * AUX[k - 5 - 2 * Nn];
             lpc += -(0.5 * nu + 1.0) * qk - 0.5 * nu / ek + qk;
           }
         }
       }
+      pg.a[s] = gk;
+      ca.a[s] = ck;
+    }
+    st(V_PG, pg);
+    st(V_CA, ca);
+    const double lp = wave_sum(lpc);
+    if (lane == 0) {
+      Sp->pr_lp = lp;
+      Sp->pr_is2 = lik ? is2 : 0.0;
+    }
+  }
+
+  // After the sweep: reduce the 8 waves' partial sums (gather_sums) and complete
+  // lp / grad from what prior_part left in LDS.  s0 = sum of squared residuals.
+  __device__ double finish_grad(V& g, double& s0) const {
+    gather_sums();
+    const int Nn = Pr().Nn, fam = Pr().family, D = Pr().D;
+    const bool lik = (Pr().prior_PD == 0);
+    const double S0 = lik ? SUMS[0] : 0.0;
+    double famsum = 0.0;
+    if (fam == FAM_HORSESHOE && lik)
+      famsum = wave_sum(lane < Nn ? AUX[64 + lane] * SUMS[4 + lane] : 0.0);
+    const V pg = ld(V_PG), ca = ld(V_CA);
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) {
+      const int k = idx(s);
+      double gk = pg.a[s];
+      if (lik && k < D) {
+        gk = fma(ca.a[s], SUMS[sidx(k)], gk);
+        if (fam == FAM_HORSESHOE && (k == 3 + Nn || k == 4 + Nn))
+          gk = fma(k == 3 + Nn ? 1.0 : 0.5, famsum, gk);
+      }
       g.a[s] = gk;
     }
-    double lp = wave_sum(lpc);
-    if (bad || !(fabs(lp) <= DBL_MAX)) lp = -INFINITY;
+    s0 = lik ? S0 : NAN;
+    double lp = fma(-0.5 * S0, Sp->pr_is2, Sp->pr_lp);
+    if ((lik && !(S0 <= DBL_MAX)) || !(fabs(lp) <= DBL_MAX)) lp = -INFINITY;
     return lp;
   }
 
@@ -653,19 +802,48 @@ struct Chain {
   enum Act : int {
     A_YIELD = 0, A_GRAD, A_INIT_STATE, A_INIT_START, A_INIT_STEP, A_SS_BEGIN, A_SS_TRIAL,
     A_SS_STEP, A_SS_FINISH, A_START_TRANSITION, A_BEGIN_SUBTREE, A_LEAF, A_END_TREE,
-    A_NEXT_TRANSITION, A_FINISH, A_LEAPFROG, A_WRITE_MP
+    A_NEXT_TRANSITION, A_FINISH, A_LEAPFROG, A_WRITE_MP, A_PRIOR
   };
 
   __device__ __forceinline__ int uni(int x) const { return __builtin_amdgcn_readfirstlane(x); }
+  // diagnostic sub-action stamps (FITOCT_STAMPS): cycles since t into prof[0][20 + i]
+  __device__ __forceinline__ void sub(int i, long long& t) const {
+    if (Pr().stamps) {
+      wave_fence();
+      const long long n = (long long)__builtin_amdgcn_s_memtime();
+      if (lane == 0) Sp->prof[0][20 + i] += n - t;
+      t = n;
+    }
+  }
+  __device__ __forceinline__ long long stamp0() const {
+    return Pr().stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  }
+
+  // runs while the gradient waves sweep the staged position: the position-only
+  // part of lp / grad, and the uniforms the coming leaf's merges will consume
+  __device__ int act_prior() {
+    prior_part();
+    if (uni(Sp->state) == ST_TREE && lane == 0) {
+      const int d = uni(Sp->depth), j = uni(Sp->leaf);
+      const uint32_t t = (uint32_t)uni(Sp->t);
+      for (int l = 0; l < d && ((j >> l) & 1); ++l)
+        Sp->u_merge[l] = uniform(key, t, TAG_MERGE | ((uint32_t)l << 8) | ((uint32_t)d << 16),
+                                 (uint32_t)j, 0u);
+      if (j == (1 << d) - 1) Sp->u_top = uniform(key, t, TAG_TOP, (uint32_t)d, 0u);
+    }
+    return A_YIELD;
+  }
 
   // a gradient arrived for CUR_Q: complete lp / grad, store them, dispatch
   __device__ int act_grad() {
-    gather_sums();
+    long long ts = stamp0();
     V g;
-    const double lp = complete(g);
+    double s0;
+    const double lp = finish_grad(g, s0);
+    sub(5, ts);
     st(V_CUR_G, g);
     Sp->cur_lp = lp;
-    Sp->cur_s2 = (Pr().prior_PD == 0) ? SUMS[0] : NAN;
+    Sp->cur_s2 = s0;
     const int stt = uni(Sp->state);
     return stt == ST_TREE ? A_LEAF : stt == ST_STEPSIZE ? A_SS_STEP : A_INIT_STEP;
   }
@@ -775,7 +953,9 @@ struct Chain {
     return A_WRITE_MP;
   }
   __device__ int act_write_mp() {
+    long long ts = stamp0();
     write_mp(ld(V_CUR_Q));
+    sub(8, ts);
     return A_YIELD;
   }
   // end_update_p with the gradient that just arrived
@@ -850,7 +1030,8 @@ struct Chain {
     Sp->end_lp[0] = Sp->end_lp[1] = Sp->smp_lp;
     Sp->end_s2[0] = Sp->end_s2[1] = Sp->smp_s2;
     st(V_RHO, p);
-    Sp->lsw = 0.0;
+    Sp->lsw_m = 0.5;   // weight of the initial point: exp(0) = 0.5 * 2^1
+    Sp->lsw_e = 1;
     Sp->n_leapfrog = 0;
     Sp->sum_metro = 0.0;
     Sp->depth = 0;
@@ -877,70 +1058,82 @@ struct Chain {
     return A_LEAPFROG;
   }
 
-  // proposal pool: at most max_depth + 1 live slots (stack records + the running subtree)
-  __device__ int pool_put_cur() {   // persist the current leaf as a proposal (HBM, no wait)
-    const unsigned used = (unsigned)uni(Sp->pool_used);
+  // proposal pool: at most max_depth + 1 live slots (stack records + the running
+  // subtree).  `used` is the slot bitmask, kept in registers by the caller.
+  __device__ int pool_put(unsigned& used, const V& p, double lp, double s2) const {
     const int sl = __builtin_ctz(~used);
-    Sp->pool_used = (int)(used | (1u << sl));
-    const V q = ld(V_CUR_Q), p = ld(V_CUR_P), g = ld(V_CUR_G);
+    used |= 1u << sl;
+    const V q = ld(V_CUR_Q), g = ld(V_CUR_G);
+    AS_GLB double* dq = pslot(sl, P_Q);
+    AS_GLB double* dp = pslot(sl, P_P);
+    AS_GLB double* dg = pslot(sl, P_G);
 #pragma unroll
-    for (int s = 0; s < PPL; ++s) {
-      pslot(sl, P_Q)[idx(s)] = q.a[s];
-      pslot(sl, P_P)[idx(s)] = p.a[s];
-      pslot(sl, P_G)[idx(s)] = g.a[s];
+    for (int s = 0; s < PPL; ++s) {   // HBM stores, never waited on
+      dq[idx(s)] = q.a[s];
+      dp[idx(s)] = p.a[s];
+      dg[idx(s)] = g.a[s];
     }
-    Sp->pool_lp[sl] = Sp->cur_lp;
-    Sp->pool_s2[sl] = Sp->cur_s2;
+    Sp->pool_lp[sl] = lp;
+    Sp->pool_s2[sl] = s2;
     return sl;
-  }
-  __device__ void pool_free(int sl) {
-    if (sl >= 0) Sp->pool_used = (int)((unsigned)Sp->pool_used & ~(1u << sl));
   }
 
   // one leaf of base_nuts::build_tree, followed by every merge it completes and,
-  // when the subtree of depth d is complete, the top-level merge of the transition
+  // when the subtree of depth d is complete, the top-level merge of the transition.
+  // Chain scalars are read once into registers and written back once, so the
+  // action costs a handful of LDS round trips instead of one per field.
   __device__ int act_leaf() {
-    const double e = Sp->lf_e;
-    const V p = finish_leapfrog(e);
-    const V minv = ld(V_MINV);
-    Sp->n_leapfrog += 1;
-    double h = -Sp->cur_lp + kin(p, minv);
+    long long ts = stamp0();
+    const double e = Sp->lf_e, cur_lp = Sp->cur_lp, cur_s2 = Sp->cur_s2, H0 = Sp->H0;
+    const double sum_metro0 = Sp->sum_metro;
+    const int d = uni(Sp->depth), j = uni(Sp->leaf), nlf = uni(Sp->n_leapfrog);
+    unsigned used = (unsigned)uni(Sp->pool_used);
+    V p = ld(V_CUR_P);
+    const V g = ld(V_CUR_G), minv = ld(V_MINV);
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) p.a[s] = fma(0.5 * e, g.a[s], p.a[s]);   // end_update_p
+    st(V_CUR_P, p);
+    Sp->n_leapfrog = nlf + 1;
+    double h = -cur_lp + kin(p, minv);
     if (isnan(h)) h = INFINITY;
-    if (h - Sp->H0 > 1000.0) Sp->divergent = 1;
-    const double wl = Sp->H0 - h;
-    Sp->sum_metro += (wl > 0.0) ? 1.0 : exp(wl);
-    if (uni(Sp->divergent)) return A_END_TREE;
+    sub(0, ts);
+    const double wl = H0 - h;
+    const XF wleaf = xf_exp(wl);
+    Sp->sum_metro = sum_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
+    sub(1, ts);
+    if (h - H0 > 1000.0) {   // divergent: the transition ends here
+      Sp->divergent = 1;
+      return A_END_TREE;
+    }
 
     V Tpb = p, Trho = p;
-    double Tlsw = wl;
+    XF Tw = wleaf;
     int Tprop = -1;   // -1: the current leaf (CUR); else a pool slot
-    const int d = uni(Sp->depth), j = uni(Sp->leaf);
-    const uint32_t t = (uint32_t)uni(Sp->t);
 #pragma unroll 1
     for (int l = 0; l < d; ++l) {
       if (((j >> l) & 1) == 0) {   // push T as the init subtree of level l+1
         lst(l, K_PBEG, Tpb);
         lst(l, K_PEND, p);
         lst(l, K_RHO, Trho);
-        Sp->st_lsw[l] = Tlsw;
-        Sp->st_prop[l] = (Tprop < 0) ? pool_put_cur() : Tprop;
+        Sp->st_w_m[l] = Tw.m;
+        Sp->st_w_e[l] = Tw.e;
+        Sp->st_prop[l] = (Tprop < 0) ? pool_put(used, p, cur_lp, cur_s2) : Tprop;
+        sub(10, ts);
         break;
       }
       // merge init I = level l with final T (base_nuts::build_tree at depth l+1)
       const V Ipb = lld(l, K_PBEG), Ipe = lld(l, K_PEND), Irho = lld(l, K_RHO);
-      const double Ilsw = Sp->st_lsw[l];
+      const XF Iw{Sp->st_w_m[l], Sp->st_w_e[l]};
+      const double um = Sp->u_merge[l];   // drawn by act_prior
       const int Iprop = uni(Sp->st_prop[l]);
-      const double lsw_sub = lse(Ilsw, Tlsw);
-      bool take_final = true;
-      if (!(Tlsw > lsw_sub)) {
-        const double u = uniform(key, t, TAG_MERGE | ((uint32_t)l << 8) | ((uint32_t)d << 16),
-                                 (uint32_t)j, 0u);
-        take_final = u < exp(Tlsw - lsw_sub);
-      }
+      sub(6, ts);
+      const XF Sw = xf_add(Iw, Tw);
+      const bool take_final = xf_gt(Tw, Sw) || xf_u_below(um, Tw, Sw);
+      sub(7, ts);
       if (take_final) {
-        pool_free(Iprop);
+        used &= ~(1u << Iprop);
       } else {
-        pool_free(Tprop);
+        if (Tprop >= 0) used &= ~(1u << Tprop);
         Tprop = Iprop;
       }
       V rsub, rx, ry;
@@ -950,47 +1143,51 @@ struct Chain {
         rx.a[s] = Irho.a[s] + Tpb.a[s];
         ry.a[s] = Trho.a[s] + Ipe.a[s];
       }
-      const bool okc = crit(Ipb, p, rsub, minv) && crit(Ipb, Tpb, rx, minv) &&
-                       crit(Ipe, p, ry, minv);
+      const bool okc = crit3(Ipb, p, rsub, Ipb, Tpb, rx, Ipe, p, ry, minv);
+      sub(9, ts);
       Tpb = Ipb;
       Trho = rsub;
-      Tlsw = lsw_sub;
-      if (!okc) return A_END_TREE;
+      Tw = Sw;
+      if (!okc) {
+        Sp->pool_used = (int)used;
+        return A_END_TREE;
+      }
     }
+    sub(2, ts);
     if (j != (1 << d) - 1) {
+      Sp->pool_used = (int)used;
       Sp->leaf = j + 1;
       return A_LEAPFROG;
     }
     // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
     const int dir = uni(Sp->dir);
+    const XF Ww{Sp->lsw_m, Sp->lsw_e};
+    const double u_top = Sp->u_top;
     const int eq = dir ? V_E1_Q : V_E0_Q;
     copyv(eq, V_CUR_Q);
     st(eq + 1, p);
-    copyv(eq + 2, V_CUR_G);
-    Sp->end_lp[dir] = Sp->cur_lp;
-    Sp->end_s2[dir] = Sp->cur_s2;
+    st(eq + 2, g);
+    Sp->end_lp[dir] = cur_lp;
+    Sp->end_s2[dir] = cur_s2;
     Sp->depth = d + 1;
-    bool take;
-    if (Tlsw > Sp->lsw) {
-      take = true;
-    } else {
-      const double u = uniform(key, t, TAG_TOP, (uint32_t)d, 0u);
-      take = u < exp(Tlsw - Sp->lsw);
-    }
+    const bool take = xf_gt(Tw, Ww) || xf_u_below(u_top, Tw, Ww);   // u_top: drawn by act_prior
     if (take) {
       if (Tprop < 0) {
         copyv(V_SMP_Q, V_CUR_Q);
         st(V_SMP_P, p);
-        copyv(V_SMP_G, V_CUR_G);
-        Sp->smp_lp = Sp->cur_lp;
-        Sp->smp_s2 = Sp->cur_s2;
+        st(V_SMP_G, g);
+        Sp->smp_lp = cur_lp;
+        Sp->smp_s2 = cur_s2;
       } else {
+        const AS_GLB double* sq = pslot(Tprop, P_Q);
+        const AS_GLB double* sp = pslot(Tprop, P_P);
+        const AS_GLB double* sg = pslot(Tprop, P_G);
         V q2, p2, g2;
 #pragma unroll
         for (int s = 0; s < PPL; ++s) {
-          q2.a[s] = pslot(Tprop, P_Q)[idx(s)];
-          p2.a[s] = pslot(Tprop, P_P)[idx(s)];
-          g2.a[s] = pslot(Tprop, P_G)[idx(s)];
+          q2.a[s] = sq[idx(s)];
+          p2.a[s] = sp[idx(s)];
+          g2.a[s] = sg[idx(s)];
         }
         st(V_SMP_Q, q2);
         st(V_SMP_P, p2);
@@ -999,8 +1196,12 @@ struct Chain {
         Sp->smp_s2 = Sp->pool_s2[Tprop];
       }
     }
-    pool_free(Tprop);
-    Sp->lsw = lse(Sp->lsw, Tlsw);
+    if (Tprop >= 0) used &= ~(1u << Tprop);
+    Sp->pool_used = (int)used;
+    sub(3, ts);
+    const XF Wn = xf_add(Ww, Tw);
+    Sp->lsw_m = Wn.m;
+    Sp->lsw_e = Wn.e;
     const V far = ld(dir ? V_E0_P : V_E1_P), near = ld(V_PNEAR), rho = ld(V_RHO);
     V rtot, rx, ry;
 #pragma unroll
@@ -1009,9 +1210,9 @@ struct Chain {
       rx.a[s] = rho.a[s] + Tpb.a[s];
       ry.a[s] = Trho.a[s] + near.a[s];
     }
-    const bool persist = crit(far, p, rtot, minv) && crit(far, Tpb, rx, minv) &&
-                         crit(near, p, ry, minv);
+    const bool persist = crit3(far, p, rtot, far, Tpb, rx, near, p, ry, minv);
     st(V_RHO, rtot);
+    sub(4, ts);
     if (!persist || d + 1 >= Pr().max_depth) return A_END_TREE;
     return A_BEGIN_SUBTREE;
   }
@@ -1020,7 +1221,7 @@ struct Chain {
     const int t = Sp->t, W = Pr().warmup;
     if (t < W && !Pr().save_warmup) return;
     const int it = Pr().save_warmup ? t : t - W;
-    double* rec = Pr().draws + ((size_t)lc * Pr().iters_saved + it) * Pr().ncols;
+    AS_GLB double* rec = (AS_GLB double*)Pr().draws + ((size_t)lc * Pr().iters_saved + it) * Pr().ncols;
     const V q = ld(V_SMP_Q);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
@@ -1139,14 +1340,14 @@ struct Chain {
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
       if (k < Pr().D) {
-        if (Pr().fin_q) Pr().fin_q[(size_t)lc * Pr().D + k] = q.a[s];
-        if (Pr().fin_minv) Pr().fin_minv[(size_t)lc * Pr().D + k] = minv.a[s];
+        if (Pr().fin_q) ((AS_GLB double*)Pr().fin_q)[(size_t)lc * Pr().D + k] = q.a[s];
+        if (Pr().fin_minv) ((AS_GLB double*)Pr().fin_minv)[(size_t)lc * Pr().D + k] = minv.a[s];
       }
     }
     if (lane == 0) {
-      if (Pr().fin_eps) Pr().fin_eps[lc] = Sp->eps;
-      if (Pr().chain_status) Pr().chain_status[lc] = Sp->status;
-      if (Pr().leapfrogs) Pr().leapfrogs[lc] = Sp->leapfrogs;
+      if (Pr().fin_eps) ((AS_GLB double*)Pr().fin_eps)[lc] = Sp->eps;
+      if (Pr().chain_status) ((AS_GLB int*)Pr().chain_status)[lc] = Sp->status;
+      if (Pr().leapfrogs) ((AS_GLB long long*)Pr().leapfrogs)[lc] = Sp->leapfrogs;
     }
     return A_YIELD;
   }
@@ -1157,6 +1358,12 @@ struct Chain {
       a = uni(a);
       // opaque per action: no jump threading across actions, and no address or
       // kernarg load hoisted out of the action loop (keeps register pressure local)
+      {   // keep the block pointer provably wave-uniform (SGPRs) in every variant
+        const uint64_t pv = (uint64_t)pp;
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pv);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(pv >> 32));
+        pp = (KPc*)(((uint64_t)hi << 32) | lo);
+      }
       asm volatile("" : "+s"(a), "+s"(pp));
       if (a == A_YIELD) break;
       const bool prof = Pr().stamps != nullptr;
@@ -1179,6 +1386,7 @@ struct Chain {
         case A_FINISH: a = act_finish(); break;
         case A_LEAPFROG: a = act_leapfrog(); break;
         case A_WRITE_MP: a = act_write_mp(); break;
+        case A_PRIOR: a = act_prior(); break;
         default: a = A_YIELD; break;
       }
       if (prof) {
@@ -1195,7 +1403,7 @@ struct Chain {
 // kernels
 // ---------------------------------------------------------------------------
 template <int PPL, int NNP>
-__device__ __forceinline__ void load_kinv(const KParams& P, const Lds<PPL>& L, int tid) {
+__device__ __forceinline__ void load_kinv(KPc& P, const Lds<PPL>& L, int tid) {
   if (P.mode == MODE_POLY) {  // zero-padded to NNP x NNP so the device loops are fixed-size
     const int Nn = P.Nn;
     for (int i = tid; i < NNP * NNP; i += TPB) {
@@ -1225,15 +1433,15 @@ constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded,
 // so the sampler latency of one chain hides behind the sweeps of the others.
 template <class R, int BPT, int NNP, int PPL, int MODE>
 __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict__ Pg) {
-  const KParams& P = *Pg;   // device-resident parameter block: uniform s_load reads
+  KPc& P = *(KPc*)Pg;   // device-resident parameter block: uniform s_load reads
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds<PPL> L{smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
+  const Lds<PPL> L{(AS_LDS char*)smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c0 = blockIdx.x * P.G;
   const int nct = min(P.G, P.chains - c0);
   __shared__ unsigned long long ring[RINGN];
-  __shared__ int q_reserve, n_active, grad_cnt[GMAX], pad_[2];
+  __shared__ int q_reserve, n_active, grad_cnt[GMAX];
 
   load_kinv<PPL, NNP>(P, L, tid);
   if (tid == 0) {
@@ -1245,7 +1453,8 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
   __syncthreads();
 
   const bool stamp = (P.stamps != nullptr) && lane == 0 && (wave == 0 || wave == NGW);
-  long long t_busy = 0, n_items = 0, t_begin = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  long long t_busy = 0, n_items = 0, t_wait = 0;
+  long long t_begin = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
   if (wave < NGW) {  // ------------------------- gradient waves
     Bins<R, BPT, NNP, MODE> bins;
     bins.load(P, tid);
@@ -1282,12 +1491,32 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
     __builtin_amdgcn_s_setprio(3);
     const int c = wave - NGW;
     if (c < nct) {
-      Chain<PPL, NNP> ch(P, L, c, c0 + c, lane, nct);
+      using Ch = Chain<PPL, NNP>;
+      Ch ch(P, L, c, c0 + c, lane, nct);
       long long epoch = 0;
-      int a = Chain<PPL, NNP>::A_INIT_STATE;
+      int a = Ch::A_INIT_STATE;
+      bool in_sweep = false;   // the last run() was A_PRIOR, overlapping the chain's sweep
+      // ONE call site of the action machine (it is inlined once, not per caller)
       for (;;) {
         const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
-        ch.run(a);   // ends with the next position staged in MP[c] (or the chain done)
+        ch.run(a);
+        if (in_sweep) {
+          in_sweep = false;
+          long long spins = 0;
+          const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
+            if (++spins > SPIN_LIMIT) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (stamp) t_wait += (long long)__builtin_amdgcn_s_memtime() - w0;
+          if (spins > SPIN_LIMIT) {
+            ch.Sp->status = ERR_TIMEOUT;
+            a = Ch::A_FINISH;
+          } else {
+            a = Ch::A_GRAD;
+          }
+          continue;
+        }
         if (stamp) {
           t_busy += (long long)__builtin_amdgcn_s_memtime() - s0;
           ++n_items;
@@ -1295,8 +1524,8 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
         if (ch.Sp->state == ST_DONE) break;
         if (epoch >= P.max_steps) {   // termination guarantee: report, never hang
           ch.Sp->status = ERR_TIMEOUT;
-          ch.run(Chain<PPL, NNP>::A_FINISH);
-          break;
+          a = Ch::A_FINISH;
+          continue;
         }
         // enqueue chain c: sequence number from a ring-wide counter, one 64-bit store
         if (lane == 0) {
@@ -1305,43 +1534,38 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
                            __ATOMIC_RELAXED);
         }
         ++epoch;
-        long long spins = 0;
-        while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
-          if (++spins > SPIN_LIMIT) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (spins > SPIN_LIMIT) {
-          ch.Sp->status = ERR_TIMEOUT;
-          ch.run(Chain<PPL, NNP>::A_FINISH);
-          break;
-        }
-        a = Chain<PPL, NNP>::A_GRAD;
+        // position-only work (prior terms, next merges' uniforms) overlaps the sweep
+        a = Ch::A_PRIOR;
+        in_sweep = true;
       }
       wave_fence();
       if (lane == 0) atomicSub(&n_active, 1);
     }
   }
   if (stamp) {
-    long long* o = P.stamps + (size_t)blockIdx.x * 40;
+    AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)blockIdx.x * NSTAMP;
     if (wave == 0) {
       o[0] = n_items;
       o[1] = t_busy;
       o[3] = (long long)__builtin_amdgcn_s_memtime() - t_begin;
     } else {
       o[2] = t_busy;
+      o[40] = t_wait;
+      o[41] = n_items;
       for (int k = 0; k < 18; ++k) {
         o[4 + k] = L.cs(0).prof[0][k];
         o[22 + k] = L.cs(0).prof[1][k];
       }
+      for (int k = 0; k < 12; ++k) o[48 + k] = L.cs(0).prof[0][20 + k];
     }
   }
 }
 
 template <class R, int BPT, int NNP, int PPL, int MODE>
 __global__ void __launch_bounds__(TPB, 3) logp_kernel(const KParams* __restrict__ Pg) {
-  const KParams& P = *Pg;
+  KPc& P = *(KPc*)Pg;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds<PPL> L{smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
+  const Lds<PPL> L{(AS_LDS char*)smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c0 = blockIdx.x * P.G;
@@ -1357,7 +1581,7 @@ __global__ void __launch_bounds__(TPB, 3) logp_kernel(const KParams* __restrict_
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = s * WAVE + lane;
-      q.a[s] = (k < P.D) ? P.q_in[(size_t)(c0 + c) * P.D + k] : 0.0;
+      q.a[s] = (k < P.D) ? ((const AS_GLB double*)P.q_in)[(size_t)(c0 + c) * P.D + k] : 0.0;
     }
     if (lane < NSLOT) ch.SUMS[lane] = 0.0;
     ch.write_mp(q);
@@ -1372,18 +1596,20 @@ __global__ void __launch_bounds__(TPB, 3) logp_kernel(const KParams* __restrict_
   __syncthreads();
   if (wave >= NGW && c < nct) {
     Chain<PPL, NNP> ch(P, L, c, c0 + c, lane, nct);
-    ch.gather_sums();
+    ch.prior_part();
+    wave_fence();
     Vd<PPL> g;
-    const double lp = ch.complete(g);
+    double s0;
+    const double lp = ch.finish_grad(g, s0);
     const size_t pt = (size_t)(c0 + c);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = s * WAVE + lane;
-      if (k < P.D) P.grad_out[pt * P.D + k] = g.a[s];
+      if (k < P.D) ((AS_GLB double*)P.grad_out)[pt * P.D + k] = g.a[s];
     }
     if (lane == 0) {
-      P.lp_out[pt] = lp;
-      if (P.s2_out) P.s2_out[pt] = (P.prior_PD == 0) ? ch.SUMS[0] : NAN;
+      ((AS_GLB double*)P.lp_out)[pt] = lp;
+      if (P.s2_out) ((AS_GLB double*)P.s2_out)[pt] = s0;
     }
   }
 }

@@ -358,12 +358,47 @@ static void leapfrog(nuts_ctx* c, ps_point* z, double e) {
   z->lp = logp_grad(c->m, z->q, z->g, &z->s2, c->work);
   for (int k = 0; k < D; ++k) z->p[k] += 0.5 * e * z->g[k];
 }
-static double log_sum_exp(double a, double b) {
-  if (a == -INFINITY) return b;
-  if (b == -INFINITY) return a;
-  const double mx = a > b ? a : b;
-  return mx + log1p(exp(-fabs(a - b)));
+/* Multinomial weights exp(H0 - H) as extended-exponent floats m * 2^e
+ * (m in [1/2, 1) or 0).  Stan keeps log weights and merges them with
+ * log_sum_exp; the linear form is the same arithmetic up to rounding, cannot
+ * overflow, and is what the HIP sampler uses (nuts_device.hip, struct XF), so
+ * both take the same merge decisions. */
+typedef struct {
+  double m;
+  int e;
+} xf;
+static xf xf_norm(double m, int e) {
+  int k;
+  const double f = frexp(m, &k);
+  xf r = {f, f == 0.0 ? 0 : e + k};
+  return r;
 }
+static xf xf_exp(double x) {
+  if (x > -700.0 && x < 700.0) return xf_norm(exp(x), 0);
+  if (!(x > -INFINITY)) {
+    xf z = {0.0, 0};
+    return z;
+  }
+  const double k = floor(x * 1.4426950408889634);
+  return xf_norm(exp(fma(-k, 0.6931471805599453, x)), (int)k);
+}
+static xf xf_add(xf a, xf b) {
+  if (a.m == 0.0) return b;
+  if (b.m == 0.0) return a;
+  const int e = a.e > b.e ? a.e : b.e;
+  return xf_norm(ldexp(a.m, a.e - e) + ldexp(b.m, b.e - e), e);
+}
+static int xf_gt(xf a, xf b) {
+  if (a.m == 0.0) return 0;
+  if (b.m == 0.0) return 1;
+  return a.e != b.e ? a.e > b.e : a.m > b.m;
+}
+static int xf_u_below(double u, xf a, xf b) { /* u < a / b */
+  if (b.m == 0.0) return 0;
+  return ldexp(u * b.m, b.e - a.e) < a.m;
+}
+static double xf_val(xf a) { return ldexp(a.m, a.e); }
+
 /* compute_criterion on p_sharp = minv .* p */
 static int criterion(const double* pm, const double* pp, const double* rho, const double* minv,
                      int D) {
@@ -378,7 +413,7 @@ static int criterion(const double* pm, const double* pp, const double* rho, cons
 /* base_nuts::build_tree.  Vectors: p_beg/p_end (momenta at the subtree ends),
  * rho (momentum sum, accumulated into), z_propose (out).  Returns validity. */
 static int build_tree(nuts_ctx* c, int depth, ps_point* z_propose, double* p_beg, double* p_end,
-                      double* rho, double sign, double* log_sum_weight) {
+                      double* rho, double sign, xf* sum_weight) {
   const int D = c->D;
   if (depth == 0) {
     leapfrog(c, &c->z, sign * c->eps);
@@ -386,9 +421,10 @@ static int build_tree(nuts_ctx* c, int depth, ps_point* z_propose, double* p_beg
     double h = hamiltonian(&c->z, c->minv, D);
     if (isnan(h)) h = INFINITY;
     if (h - c->H0 > 1000.0) c->divergent = 1;
-    *log_sum_weight = log_sum_exp(*log_sum_weight, c->H0 - h);
+    const xf wleaf = xf_exp(c->H0 - h);
+    *sum_weight = xf_add(*sum_weight, wleaf);
     if (c->H0 - h > 0) c->sum_metro += 1.0;
-    else c->sum_metro += exp(c->H0 - h);
+    else c->sum_metro += xf_val(wleaf);
     pt_copy(z_propose, &c->z, D);
     for (int k = 0; k < D; ++k) {
       rho[k] += c->z.p[k];
@@ -399,7 +435,7 @@ static int build_tree(nuts_ctx* c, int depth, ps_point* z_propose, double* p_beg
     return !c->divergent;
   }
   /* initial subtree */
-  double lsw_init = -INFINITY;
+  xf w_init = {0.0, 0};
   double* p_init_end = (double*)calloc(D, sizeof(double));
   double* rho_init = (double*)calloc(D, sizeof(double));
   double* p_final_beg = (double*)calloc(D, sizeof(double));
@@ -407,21 +443,21 @@ static int build_tree(nuts_ctx* c, int depth, ps_point* z_propose, double* p_beg
   double* tmp = (double*)calloc(D, sizeof(double));
   ps_point z_final;
   pt_alloc(&z_final, D);
-  int ok = build_tree(c, depth - 1, z_propose, p_beg, p_init_end, rho_init, sign, &lsw_init);
+  int ok = build_tree(c, depth - 1, z_propose, p_beg, p_init_end, rho_init, sign, &w_init);
   if (ok) {
-    double lsw_final = -INFINITY;
-    ok = build_tree(c, depth - 1, &z_final, p_final_beg, p_end, rho_final, sign, &lsw_final);
+    xf w_final = {0.0, 0};
+    ok = build_tree(c, depth - 1, &z_final, p_final_beg, p_end, rho_final, sign, &w_final);
     if (ok) {
-      const double lsw_sub = log_sum_exp(lsw_init, lsw_final);
-      *log_sum_weight = log_sum_exp(*log_sum_weight, lsw_sub);
-      if (lsw_final > lsw_sub) {
+      const xf w_sub = xf_add(w_init, w_final);
+      *sum_weight = xf_add(*sum_weight, w_sub);
+      if (xf_gt(w_final, w_sub)) {
         pt_copy(z_propose, &z_final, D);
       } else {
         /* the merge completes at the subtree's last leaf: (level, top depth, leaf) */
         const double u = unif(c->key, c->t,
                               T_MERGE | ((uint32_t)(depth - 1) << 8) | ((uint32_t)c->top_depth << 16),
                               (uint32_t)(c->leaf - 1), 0u);
-        if (u < exp(lsw_final - lsw_sub)) pt_copy(z_propose, &z_final, D);
+        if (xf_u_below(u, w_final, w_sub)) pt_copy(z_propose, &z_final, D);
       }
       for (int k = 0; k < D; ++k) {
         const double rs = rho_init[k] + rho_final[k];
@@ -474,7 +510,7 @@ static void transition(nuts_ctx* c, ps_point* z_sample, int max_depth, trans_inf
   for (int k = 0; k < D; ++k) {
     p_fwd_fwd[k] = p_fwd_bck[k] = p_bck_fwd[k] = p_bck_bck[k] = rho[k] = z_sample->p[k];
   }
-  double log_sum_weight = 0.0;
+  xf sum_weight = {0.5, 1}; /* exp(0): the initial point */
   c->H0 = hamiltonian(z_sample, c->minv, D);
   c->n_leapfrog = 0;
   c->sum_metro = 0.0;
@@ -482,7 +518,7 @@ static void transition(nuts_ctx* c, ps_point* z_sample, int max_depth, trans_inf
   int depth = 0;
   while (depth < max_depth) {
     for (int k = 0; k < D; ++k) rho_fwd[k] = rho_bck[k] = 0.0;
-    double lsw_sub = -INFINITY;
+    xf w_sub = {0.0, 0};
     int valid;
     c->top_depth = depth;
     c->leaf = 0;
@@ -490,24 +526,24 @@ static void transition(nuts_ctx* c, ps_point* z_sample, int max_depth, trans_inf
       pt_copy(&c->z, &z_fwd, D);
       memcpy(rho_bck, rho, sizeof(double) * D);
       memcpy(p_bck_fwd, p_fwd_fwd, sizeof(double) * D);
-      valid = build_tree(c, depth, &z_propose, p_fwd_bck, p_fwd_fwd, rho_fwd, 1.0, &lsw_sub);
+      valid = build_tree(c, depth, &z_propose, p_fwd_bck, p_fwd_fwd, rho_fwd, 1.0, &w_sub);
       pt_copy(&z_fwd, &c->z, D);
     } else {
       pt_copy(&c->z, &z_bck, D);
       memcpy(rho_fwd, rho, sizeof(double) * D);
       memcpy(p_fwd_bck, p_bck_bck, sizeof(double) * D);
-      valid = build_tree(c, depth, &z_propose, p_bck_fwd, p_bck_bck, rho_bck, -1.0, &lsw_sub);
+      valid = build_tree(c, depth, &z_propose, p_bck_fwd, p_bck_bck, rho_bck, -1.0, &w_sub);
       pt_copy(&z_bck, &c->z, D);
     }
     if (!valid) break;
     ++depth;
-    if (lsw_sub > log_sum_weight) {
+    if (xf_gt(w_sub, sum_weight)) {
       pt_copy(z_sample, &z_propose, D);
     } else {
       const double u = unif(c->key, c->t, T_TOP, (uint32_t)(depth - 1), 0u);
-      if (u < exp(lsw_sub - log_sum_weight)) pt_copy(z_sample, &z_propose, D);
+      if (xf_u_below(u, w_sub, sum_weight)) pt_copy(z_sample, &z_propose, D);
     }
-    log_sum_weight = log_sum_exp(log_sum_weight, lsw_sub);
+    sum_weight = xf_add(sum_weight, w_sub);
     for (int k = 0; k < D; ++k) rho[k] = rho_bck[k] + rho_fwd[k];
     int persist = criterion(p_bck_bck, p_fwd_fwd, rho, c->minv, D);
     for (int k = 0; k < D; ++k) tmp[k] = rho_bck[k] + p_fwd_bck[k];
