@@ -3,6 +3,7 @@ shared object sits next to this file so it travels with the repository
 snapshot to the GPU box.
 
     python -m fitoct_amd.build [--force] [--verbose]
+    FITOCT_PROFILE=1 python -m fitoct_amd.build --force   # diagnostic cycle-stamp build
 """
 from __future__ import annotations
 
@@ -20,12 +21,19 @@ LIB = os.path.join(HERE, "libfitoct.so")
 OBJDIR = os.path.join(HERE, "build")
 ARCH = os.environ.get("FITOCT_ARCH", "gfx950")
 
+_KERNEL = [f"--offload-arch={ARCH}", "-O3", "-std=c++17"]
 SOURCES = [
-    # (source, compiler, flags)
-    ("nuts_device.hip", "hipcc", [f"--offload-arch={ARCH}", "-O3", "-std=c++17"]),
-    ("fitoct_api.cpp", "hipcc", [f"--offload-arch={ARCH}", "-O2", "-std=c++17"]),
-    ("host_model.cpp", "g++", ["-O2", "-std=c++17"]),
+    # (object name, source, compiler, flags).  The sampler source is compiled once
+    # per prior family (the family is a template parameter of the kernels).
+    ("nuts_normal", "nuts_device.hip", "hipcc", _KERNEL + ["-DFITOCT_FAMILY=0"]),
+    ("nuts_lasso", "nuts_device.hip", "hipcc", _KERNEL + ["-DFITOCT_FAMILY=1"]),
+    ("nuts_horseshoe", "nuts_device.hip", "hipcc", _KERNEL + ["-DFITOCT_FAMILY=2"]),
+    ("fitoct_api", "fitoct_api.cpp", "hipcc", [f"--offload-arch={ARCH}", "-O2", "-std=c++17"]),
+    ("host_model", "host_model.cpp", "g++", ["-O2", "-std=c++17"]),
 ]
+# FITOCT_PROFILE=1: a diagnostic build whose kernels record cycle stamps
+# (read with FITOCT_STAMPS=1); production builds carry no timing code.
+PROFILE = os.environ.get("FITOCT_PROFILE", "0") not in ("", "0")
 HEADERS = ["kernel_params.h", "philox.h", "host_internal.h"]
 
 
@@ -36,8 +44,16 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm required to build libfitoct)")
 
 
+def _flags_file() -> str:
+    return os.path.join(OBJDIR, "flags.txt")
+
+
+def _flags() -> str:
+    return f"arch={ARCH} profile={int(PROFILE)}"
+
+
 def _newest_input() -> float:
-    paths = [os.path.join(CSRC, s) for s, _, _ in SOURCES]
+    paths = [os.path.join(CSRC, s) for _, s, _, _ in SOURCES]
     paths += [os.path.join(CSRC, h) for h in HEADERS]
     paths += [os.path.join(INCLUDE, "fitoct.h"), os.path.abspath(__file__)]
     return max(os.path.getmtime(p) for p in paths)
@@ -45,14 +61,18 @@ def _newest_input() -> float:
 
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile every translation unit and link ``fitoct_amd/libfitoct.so``."""
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_input():
+    same_flags = os.path.exists(_flags_file()) and open(_flags_file()).read() == _flags()
+    if (not force and same_flags and os.path.exists(LIB)
+            and os.path.getmtime(LIB) >= _newest_input()):
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)
     hipcc = _hipcc()
 
     def compile_one(item):
-        src, cc, flags = item
-        obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+        name, src, cc, flags = item
+        obj = os.path.join(OBJDIR, name + ".o")
+        if PROFILE and cc == "hipcc":
+            flags = flags + ["-DFITOCT_PROFILE=1"]
         exe = hipcc if cc == "hipcc" else (shutil.which("g++") or "g++")
         cmd = [exe, *flags, "-fPIC", "-Wall", f"-I{INCLUDE}", f"-I{CSRC}",
                "-I/opt/rocm/include", "-c", os.path.join(CSRC, src), "-o", obj]
@@ -73,6 +93,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB)
+    with open(_flags_file(), "w") as f:
+        f.write(_flags())
     return LIB
 
 

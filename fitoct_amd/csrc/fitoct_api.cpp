@@ -17,8 +17,22 @@
 #include "kernel_params.h"
 
 namespace fitoct {
-hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P, const KParams* dP,
-                  int tiles, hipStream_t st);
+hipError_t launch_family_0(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
+                           const KParams* dP, int tiles, hipStream_t st);
+hipError_t launch_family_1(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
+                           const KParams* dP, int tiles, hipStream_t st);
+hipError_t launch_family_2(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
+                           const KParams* dP, int tiles, hipStream_t st);
+// the sampler is compiled per prior family (nuts_device.hip, -DFITOCT_FAMILY)
+inline hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
+                         const KParams* dP, int tiles, hipStream_t st) {
+  switch (P.family) {
+    case 0: return launch_family_0(logp, mixed, bpt, nnp, P, dP, tiles, st);
+    case 1: return launch_family_1(logp, mixed, bpt, nnp, P, dP, tiles, st);
+    case 2: return launch_family_2(logp, mixed, bpt, nnp, P, dP, tiles, st);
+    default: return hipErrorInvalidValue;
+  }
+}
 int lds_bytes(int ppl, int G, int max_depth);
 }  // namespace fitoct
 

@@ -61,6 +61,14 @@ namespace fitoct {
 using KPc = const AS_CST KParams;
 
 enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2 };
+
+// Cycle stamps (FITOCT_STAMPS) exist only in a profiling build
+// (FITOCT_PROFILE=1 python -m fitoct_amd.build): the production kernels carry
+// no per-action timing code at all.
+#ifndef FITOCT_PROFILE
+#define FITOCT_PROFILE 0
+#endif
+constexpr bool kProfile = FITOCT_PROFILE != 0;
 enum { ERR_INIT = -4, ERR_NUMERIC = -5, ERR_TIMEOUT = -6 };
 
 // vectors kept in LDS per chain (lane-private elements)
@@ -380,7 +388,7 @@ struct Bins {
 };
 
 // LDS carve -----------------------------------------------------------------
-// [ K^-1 (KMAX x KMAX, row stride NNP) | b (KMAX) | MP[GMAX][MPW] | PART[NGW][G][NSLOT] |
+// [ K^-1 (KMAX x KMAX, row stride NNP) | b (KMAX) | MP[GMAX][MPW] | PART[G][NGW][NSLOT] |
 //   G x chain{ ChainScalars | NVEC vectors | SUMS[NSLOT] | AUX[NAUX] | levels[max_depth][NLVL] } ]
 template <int PPL>
 struct Lds {
@@ -412,7 +420,7 @@ struct Lds {
 };
 
 // The likelihood sweep of chains [cb, ce) of the tile (gradient waves only).
-// PART[wave][c][0 .. 4+NNP) receives this wave's partial sums of chain c.
+// PART[c][wave][0 .. 4+NNP) receives this wave's partial sums of chain c.
 template <class R, int BPT, int NNP, int MODE>
 __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                               const AS_LDS double* mpall, AS_LDS double* part, const int* done,
@@ -463,7 +471,7 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
     }
     const double r = transpose_reduce32(acc, lane);
     const int idx = lane >> 1;
-    if (!(lane & 1) && idx < 4 + NNP) part[(wave * P.G + c) * NSLOT + idx] = r;
+    if (!(lane & 1) && idx < 4 + NNP) part[(c * NGW + wave) * NSLOT + idx] = r;
   }
 }
 
@@ -475,7 +483,7 @@ struct Vd {
   double a[PPL];
 };
 
-template <int PPL, int NNP>
+template <int PPL, int NNP, int FAM>
 struct Chain {
   using V = Vd<PPL>;
   static constexpr int VLEN = WAVE * PPL;
@@ -593,10 +601,11 @@ struct Chain {
       qe[k] = (k < Pr().D && is_log(k)) ? exp(q.a[s]) : q.a[s];
     }
     wave_fence();
+    long long ts = stamp0();
     if (lane < NNP) {
       double yv = 0.0, hl = 0.0;
       if (lane < Nn) {
-        if (Pr().family == FAM_HORSESHOE) {
+        if (FAM == FAM_HORSESHOE) {
           // Tests/horseShoePrior.stan:30-32
           hl = qe[5 + Nn + lane] * sqrt(qe[5 + 2 * Nn + lane]) * (qe[3 + Nn] * sqrt(qe[4 + Nn]));
           yv = qs[3 + lane] * hl;
@@ -611,6 +620,7 @@ struct Chain {
     if (lane < 3) MP[lane] = qe[lane];
     if (Pr().mode == MODE_POLY) {  // c_l = b_l (K^-1 yGP)_l ; K^-1 padded to NNP x NNP
       wave_fence();
+      sub(4, ts);
       if (lane < NNP) {
         double c = 0.0;
 #pragma unroll
@@ -622,16 +632,18 @@ struct Chain {
 
   // ------------- lp / grad completion from the reduced bin sums --------------
   __device__ void gather_sums() const {
+    long long ts = stamp0();
     if (Pr().prior_PD == 0) {
       double s = 0.0;
       if (lane < 4 + NNP) {
 #pragma unroll
-        for (int w = 0; w < NGW; ++w) s += part[(w * Pr().G + slot) * NSLOT + lane];
+        for (int w = 0; w < NGW; ++w) s += part[(slot * NGW + w) * NSLOT + lane];
       }
       if (Pr().mode == MODE_POLY) {  // B^T h = K^-1 (b .* M)
         if (lane >= 4 && lane < 4 + NNP) SUMS[lane] = s * bv[lane - 4];
         else if (lane < 4) SUMS[lane] = s;
         wave_fence();
+        sub(2, ts);
         if (lane < NNP) {
           double v = 0.0;
 #pragma unroll
@@ -639,6 +651,7 @@ struct Chain {
           s = v;
         }
         wave_fence();
+        sub(3, ts);
         if (lane < NNP) SUMS[4 + lane] = s;
       } else if (lane < 4 + NNP) {
         SUMS[lane] = s;
@@ -658,12 +671,13 @@ struct Chain {
     if (k < 3) return 1 + k;
     if (k == D - 1) return 0;
     if (k < 3 + Nn) return 4 + (k - 3);
-    if (Pr().family == FAM_HORSESHOE && k >= 5 + Nn) return 4 + ((k - 5 - Nn) % Nn);
+    if (FAM == FAM_HORSESHOE && k >= 5 + Nn) return 4 + ((k - 5 - Nn) % Nn);
     return 0;
   }
 
   __device__ void prior_part() const {
-    const int D = Pr().D, Nn = Pr().Nn, fam = Pr().family;
+    const int D = Pr().D, Nn = Pr().Nn;
+    constexpr int fam = FAM;
     const AS_LDS double* qs = QS();
     const AS_LDS double* qe = QE();
     const bool lik = (Pr().prior_PD == 0);
@@ -756,12 +770,15 @@ struct Chain {
   // lp / grad from what prior_part left in LDS.  s0 = sum of squared residuals.
   __device__ double finish_grad(V& g, double& s0) const {
     gather_sums();
-    const int Nn = Pr().Nn, fam = Pr().family, D = Pr().D;
+    long long ts = stamp0();
+    const int Nn = Pr().Nn, D = Pr().D;
+    constexpr int fam = FAM;
     const bool lik = (Pr().prior_PD == 0);
     const double S0 = lik ? SUMS[0] : 0.0;
     double famsum = 0.0;
     if (fam == FAM_HORSESHOE && lik)
       famsum = wave_sum(lane < Nn ? AUX[64 + lane] * SUMS[4 + lane] : 0.0);
+    sub(6, ts);
     const V pg = ld(V_PG), ca = ld(V_CA);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
@@ -777,6 +794,7 @@ struct Chain {
     s0 = lik ? S0 : NAN;
     double lp = fma(-0.5 * S0, Sp->pr_is2, Sp->pr_lp);
     if ((lik && !(S0 <= DBL_MAX)) || !(fabs(lp) <= DBL_MAX)) lp = -INFINITY;
+    sub(7, ts);
     return lp;
   }
 
@@ -806,9 +824,10 @@ struct Chain {
   };
 
   __device__ __forceinline__ int uni(int x) const { return __builtin_amdgcn_readfirstlane(x); }
-  // diagnostic sub-action stamps (FITOCT_STAMPS): cycles since t into prof[0][20 + i]
+  // diagnostic sub-action stamps (profiling build + FITOCT_STAMPS): cycles since t
+  // into prof[0][20 + i]
   __device__ __forceinline__ void sub(int i, long long& t) const {
-    if (Pr().stamps) {
+    if (kProfile && Pr().stamps) {
       wave_fence();
       const long long n = (long long)__builtin_amdgcn_s_memtime();
       if (lane == 0) Sp->prof[0][20 + i] += n - t;
@@ -816,7 +835,7 @@ struct Chain {
     }
   }
   __device__ __forceinline__ long long stamp0() const {
-    return Pr().stamps ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    return (kProfile && Pr().stamps) ? (long long)__builtin_amdgcn_s_memtime() : 0;
   }
 
   // runs while the gradient waves sweep the staged position: the position-only
@@ -905,7 +924,7 @@ struct Chain {
         w = 0.05;
       } else if (k < Pr().D) {
         w = 0.25;
-        if (Pr().family == FAM_NORMAL && k == 3 + Nn) base = -log(Pr().lambda_rate_eff);
+        if (FAM == FAM_NORMAL && k == 3 + Nn) base = -log(Pr().lambda_rate_eff);
       }
       const double u = uniform(key, (uint32_t)attempt, TAG_INIT, (uint32_t)k, 0u);
       q.a[s] = (k < Pr().D) ? base + Pr().init_radius * w * (2.0 * u - 1.0) : 0.0;
@@ -1118,7 +1137,6 @@ struct Chain {
         Sp->st_w_m[l] = Tw.m;
         Sp->st_w_e[l] = Tw.e;
         Sp->st_prop[l] = (Tprop < 0) ? pool_put(used, p, cur_lp, cur_s2) : Tprop;
-        sub(10, ts);
         break;
       }
       // merge init I = level l with final T (base_nuts::build_tree at depth l+1)
@@ -1126,10 +1144,8 @@ struct Chain {
       const XF Iw{Sp->st_w_m[l], Sp->st_w_e[l]};
       const double um = Sp->u_merge[l];   // drawn by act_prior
       const int Iprop = uni(Sp->st_prop[l]);
-      sub(6, ts);
       const XF Sw = xf_add(Iw, Tw);
       const bool take_final = xf_gt(Tw, Sw) || xf_u_below(um, Tw, Sw);
-      sub(7, ts);
       if (take_final) {
         used &= ~(1u << Iprop);
       } else {
@@ -1144,7 +1160,6 @@ struct Chain {
         ry.a[s] = Trho.a[s] + Ipe.a[s];
       }
       const bool okc = crit3(Ipb, p, rsub, Ipb, Tpb, rx, Ipe, p, ry, minv);
-      sub(9, ts);
       Tpb = Ipb;
       Trho = rsub;
       Tw = Sw;
@@ -1153,7 +1168,6 @@ struct Chain {
         return A_END_TREE;
       }
     }
-    sub(2, ts);
     if (j != (1 << d) - 1) {
       Sp->pool_used = (int)used;
       Sp->leaf = j + 1;
@@ -1198,7 +1212,6 @@ struct Chain {
     }
     if (Tprop >= 0) used &= ~(1u << Tprop);
     Sp->pool_used = (int)used;
-    sub(3, ts);
     const XF Wn = xf_add(Ww, Tw);
     Sp->lsw_m = Wn.m;
     Sp->lsw_e = Wn.e;
@@ -1212,7 +1225,6 @@ struct Chain {
     }
     const bool persist = crit3(far, p, rtot, far, Tpb, rx, near, p, ry, minv);
     st(V_RHO, rtot);
-    sub(4, ts);
     if (!persist || d + 1 >= Pr().max_depth) return A_END_TREE;
     return A_BEGIN_SUBTREE;
   }
@@ -1366,7 +1378,7 @@ struct Chain {
       }
       asm volatile("" : "+s"(a), "+s"(pp));
       if (a == A_YIELD) break;
-      const bool prof = Pr().stamps != nullptr;
+      const bool prof = kProfile && Pr().stamps != nullptr;
       const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
       const int a0 = a;
       switch (a) {
@@ -1431,7 +1443,7 @@ constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded,
 // until grad_cnt[c] reaches NGW * epoch and runs the sampler until it yields
 // the next position.  Chains cycle independently (no barrier after start-up),
 // so the sampler latency of one chain hides behind the sweeps of the others.
-template <class R, int BPT, int NNP, int PPL, int MODE>
+template <class R, int BPT, int NNP, int PPL, int MODE, int FAM>
 __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict__ Pg) {
   KPc& P = *(KPc*)Pg;   // device-resident parameter block: uniform s_load reads
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1452,7 +1464,7 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
   if (tid < RINGN) ring[tid] = ~0ULL;
   __syncthreads();
 
-  const bool stamp = (P.stamps != nullptr) && lane == 0 && (wave == 0 || wave == NGW);
+  const bool stamp = kProfile && (P.stamps != nullptr) && lane == 0 && (wave == 0 || wave == NGW);
   long long t_busy = 0, n_items = 0, t_wait = 0;
   long long t_begin = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
   if (wave < NGW) {  // ------------------------- gradient waves
@@ -1491,7 +1503,7 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
     __builtin_amdgcn_s_setprio(3);
     const int c = wave - NGW;
     if (c < nct) {
-      using Ch = Chain<PPL, NNP>;
+      using Ch = Chain<PPL, NNP, FAM>;
       Ch ch(P, L, c, c0 + c, lane, nct);
       long long epoch = 0;
       int a = Ch::A_INIT_STATE;
@@ -1561,7 +1573,7 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
   }
 }
 
-template <class R, int BPT, int NNP, int PPL, int MODE>
+template <class R, int BPT, int NNP, int PPL, int MODE, int FAM>
 __global__ void __launch_bounds__(TPB, 3) logp_kernel(const KParams* __restrict__ Pg) {
   KPc& P = *(KPc*)Pg;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1576,7 +1588,7 @@ __global__ void __launch_bounds__(TPB, 3) logp_kernel(const KParams* __restrict_
   __syncthreads();
   const int c = wave - NGW;
   if (wave >= NGW && c < nct) {
-    Chain<PPL, NNP> ch(P, L, c, c0 + c, lane, nct);
+    Chain<PPL, NNP, FAM> ch(P, L, c, c0 + c, lane, nct);
     Vd<PPL> q;
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
@@ -1595,7 +1607,7 @@ __global__ void __launch_bounds__(TPB, 3) logp_kernel(const KParams* __restrict_
   }
   __syncthreads();
   if (wave >= NGW && c < nct) {
-    Chain<PPL, NNP> ch(P, L, c, c0 + c, lane, nct);
+    Chain<PPL, NNP, FAM> ch(P, L, c, c0 + c, lane, nct);
     ch.prior_part();
     wave_fence();
     Vd<PPL> g;
@@ -1615,22 +1627,33 @@ __global__ void __launch_bounds__(TPB, 3) logp_kernel(const KParams* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// host-side dispatch over the template grid
+// host-side dispatch over the template grid.  This file is compiled once per
+// prior family (-DFITOCT_FAMILY=0/1/2, in parallel); the family is a template
+// parameter of the sampler so that no family branch survives in its code.
 // ---------------------------------------------------------------------------
+#ifndef FITOCT_FAMILY
+#error "compile with -DFITOCT_FAMILY=0|1|2"
+#endif
+#define FITOCT_CAT2(a, b) a##b
+#define FITOCT_CAT(a, b) FITOCT_CAT2(a, b)
+
+#if FITOCT_FAMILY == 0
 int lds_bytes(int ppl, int G, int max_depth) {
   return ppl == 1 ? Lds<1>::bytes(G, max_depth) : Lds<2>::bytes(G, max_depth);
 }
+#endif
 
 template <class R, int BPT, int NNP, int PPL, int MODE>
 static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int tiles,
                            hipStream_t st) {
+  constexpr int F = FITOCT_FAMILY;
   const int lds = Lds<PPL>::bytes(P.G, P.max_depth);
   if (logp) {
-    auto k = logp_kernel<R, BPT, NNP, PPL, MODE>;
+    auto k = logp_kernel<R, BPT, NNP, PPL, MODE, F>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP);
   } else {
-    auto k = nuts_kernel<R, BPT, NNP, PPL, MODE>;
+    auto k = nuts_kernel<R, BPT, NNP, PPL, MODE, F>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP);
   }
@@ -1660,8 +1683,9 @@ static hipError_t launch_n(bool logp, bool mixed, int bpt, const KParams& P, con
 }
 
 // P: host copy (shapes); dP: the same block already copied to device memory
-hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P, const KParams* dP,
-                  int tiles, hipStream_t st) {
+hipError_t FITOCT_CAT(launch_family_, FITOCT_FAMILY)(bool logp, bool mixed, int bpt, int nnp,
+                                                     const KParams& P, const KParams* dP,
+                                                     int tiles, hipStream_t st) {
 #ifdef FITOCT_ONE_VARIANT
   return launch_t<double, 4, 16, 1, MODE_POLY>(logp, P, dP, tiles, st);
 #else
