@@ -112,11 +112,14 @@ int invert3(const double* S, double* Si) {
 // Shapes: bins are strided over the 512 lanes of a tile's gradient waves; up to
 // 4 bins per lane keep their data in VGPRs for the whole run (MODE_POLY: 5 f64
 // values per bin; MODE_ROWS: 3 + NNP fp32 values), beyond that they are streamed.
-void choose_bins(int N, int& bpt, int& n_pad) {
-  if (N <= GT) { bpt = 1; n_pad = GT; }
-  else if (N <= 2 * GT) { bpt = 2; n_pad = 2 * GT; }
-  else if (N <= 4 * GT) { bpt = 4; n_pad = 4 * GT; }
-  else { bpt = 0; n_pad = (N + GT - 1) / GT * GT; }
+// bins per gradient lane kept in registers (0 = streamed from HBM/L2 every sweep).
+// The factorised f64 basis holds 5 values per bin, so up to 8 bins per lane fit;
+// explicit fp32 basis rows hold NNP + 3 values per bin, up to 4.
+void choose_bins(int N, int max_bpt, int& bpt, int& n_pad) {
+  bpt = 0;
+  for (int b = 1; b <= max_bpt; b *= 2)
+    if (N <= b * GT) { bpt = b; break; }
+  n_pad = bpt ? bpt * GT : (N + GT - 1) / GT * GT;
 }
 
 // MODE_POLY factors of the SE basis on the uniform grid g_l = g_0 + l*dg:
@@ -249,9 +252,6 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   pl->ppl = (D <= WAVE) ? 1 : 2;
   if (pl->nnp == 16 && pl->ppl == 2) pl->nnp = 24;  // the (24, 2) instantiation covers it
   if (pl->nnp == 24) pl->ppl = 2;
-  int n_pad;
-  choose_bins(p->N, pl->bpt, n_pad);
-
   std::vector<double> B, xg;
   if (p->B) {
     B.assign(p->B, p->B + (size_t)p->N * p->Nn);
@@ -268,8 +268,10 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
     const bool poly = !p->B && getenv("FITOCT_NO_POLY") == nullptr &&
                       build_poly(p, B, pl->nnp, ta, kinv, bv);
     mode = poly ? MODE_POLY : MODE_ROWS;
-    if (mode == MODE_ROWS) pl->bpt = 0;   // f64 rows are streamed (16 doubles per bin)
   }
+  // f64 rows (NNP doubles per bin) are always streamed
+  int n_pad;
+  choose_bins(p->N, mode == MODE_POLY ? 8 : pl->mixed ? 4 : 0, pl->bpt, n_pad);
   std::vector<char> staged;
   if (pl->mixed) stage<float>(p, B, ta, mode, n_pad, pl->nnp, staged);
   else stage<double>(p, B, ta, mode, n_pad, pl->nnp, staged);
@@ -575,7 +577,8 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
     std::vector<long long> h((size_t)NSTAMP * pl->tiles);
     HIP_TRY(hipMemcpy(h.data(), d_stamps, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
     (void)hipFree(d_stamps);
-    double steps = 0, tg = 0, tn = 0, tt = 0, smax = 0, tw = 0, nw = 0;
+    double steps = 0, tg = 0, tn = 0, tt = 0, smax = 0, tw = 0, nw = 0, tsw = 0, tno = 0;
+    double ts0 = 0, ts1 = 0;
     double act_t[18] = {0}, act_n[18] = {0};
     for (int t = 0; t < pl->tiles; ++t) {
       const long long* o = h.data() + (size_t)NSTAMP * t;
@@ -585,15 +588,24 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
       tt += o[3];
       tw += o[40];
       nw += o[41];
+      tsw += o[42];
+      tno += o[43];
+      ts0 += o[44];
+      ts1 += o[45];
       smax = std::max(smax, (double)o[0]);
       for (int a = 0; a < 18; ++a) {
         act_t[a] += o[4 + a];
         act_n[a] += o[22 + a];
       }
     }
-    double subt[12] = {0};
-    for (int t = 0; t < pl->tiles; ++t)
-      for (int k = 0; k < 12; ++k) subt[k] += h[(size_t)NSTAMP * t + 48 + k];
+    double subt[12] = {0}, wb[8] = {0};
+    for (int t = 0; t < pl->tiles; ++t) {
+      for (int k = 0; k < 8; ++k) subt[k] += h[(size_t)NSTAMP * t + 48 + k];
+      for (int k = 0; k < 8; ++k) wb[k] += h[(size_t)NSTAMP * t + 56 + k];
+    }
+    fprintf(stderr, "[fitoct stamps] gradient-wave busy per sweep by wave:");
+    for (int k = 0; k < 8; ++k) fprintf(stderr, " %.0f", wb[k] / std::max(steps, 1.0));
+    fprintf(stderr, "\n");
     fprintf(stderr, "[fitoct stamps] sub-action cycles per leaf (chain 0): ");
     for (int k = 0; k < 12; ++k)
       if (subt[k] > 0) fprintf(stderr, "s%d:%.0f ", k, subt[k] / std::max(act_n[11], 1.0));
@@ -606,8 +618,13 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
             "[fitoct stamps] tiles=%d mean sweeps/tile=%.0f max=%.0f | per sweep: grad-wave busy %.0f "
             "nuts-wave busy %.0f wall %.0f memtime ticks\n",
             pl->tiles, steps / pl->tiles, smax, tg / steps, tn / steps, tt / steps);
-    fprintf(stderr, "[fitoct stamps] chain 0 per NUTS round: busy %.0f, waiting for its gradient %.0f\n",
-            tn / std::max(nw, 1.0), tw / std::max(nw, 1.0));
+    fprintf(stderr,
+            "[fitoct stamps] chain 0 per NUTS round: busy %.0f, waiting for its gradient %.0f "
+            "(enqueue->sweep done %.0f, sweep done->resumed %.0f)\n",
+            tn / std::max(nw, 1.0), tw / std::max(nw, 1.0), tsw / std::max(nw, 1.0),
+            tno / std::max(nw, 1.0));
+    fprintf(stderr, "[fitoct stamps] enqueue -> first wave starts %.0f, last wave starts %.0f\n",
+            ts0 / std::max(nw, 1.0), ts1 / std::max(nw, 1.0));
   }
   pl->ran = true;
   return FITOCT_OK;

@@ -6,11 +6,15 @@
 namespace fitoct {
 
 constexpr int WAVE = 64;          // CDNA wavefront
-constexpr int NW = 12;            // waves per tile (workgroup): 3 per SIMD -> 168 VGPRs each
-constexpr int TPB = NW * WAVE;    // 768 threads per tile
-constexpr int NGW = 8;            // gradient waves (waves 0..7): the likelihood sweep
-constexpr int GT = NGW * WAVE;    // 512 gradient lanes; bins are strided over them
-constexpr int GMAX = NW - NGW;    // NUTS waves (8..11), one chain each: max chains per tile
+// A tile is 8 waves = 2 per SIMD (waves w and w+4 share SIMD w mod 4): one
+// gradient wave and one NUTS wave on every SIMD, 256 VGPRs each.  The sweep is
+// VALU-issue bound; one gradient wave per SIMD (rather than two) halves the
+// per-sweep cross-lane reduction work and the partial sums the NUTS wave adds.
+constexpr int NW = 8;             // waves per tile (workgroup)
+constexpr int TPB = NW * WAVE;    // 512 threads per tile
+constexpr int NGW = 4;            // gradient waves (waves 0..3): the likelihood sweep
+constexpr int GT = NGW * WAVE;    // 256 gradient lanes; bins are strided over them
+constexpr int GMAX = NW - NGW;    // NUTS waves (4..7), one chain each: max chains per tile
 constexpr int MAXDEPTH = 16;      // hard cap on max_treedepth
 constexpr int NSLOT = 32;         // reduced sums per chain (4 + NNP <= 32)
 constexpr int MPW = 32;           // model-parameter words per chain (theta[3], pad, yGP[NNP])

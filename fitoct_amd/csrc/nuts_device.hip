@@ -591,73 +591,51 @@ struct Chain {
   // theta[3] and, per basis mode, yGP (rows) or c = b .* K^-1 yGP (poly).
   // (LDS exchange: on gfx950 a v_readlane assembly of yGP measured 3x slower.)
   __device__ void write_mp(const V& q) const {
-    const int Nn = Pr().Nn;
+    const int Nn = Pr().Nn, D = Pr().D;
+    const bool poly = Pr().mode == MODE_POLY;
     AS_LDS double* qs = vec(V_QS);
     AS_LDS double* qe = vec(V_QE);
 #pragma unroll
+    for (int s = 0; s < PPL; ++s) qs[idx(s)] = q.a[s];
+    wave_fence();   // q of every lane visible: the yGP lanes start at once, in parallel with
+                    // the constrained values below
+    double yv = 0.0, hl = 0.0, u = 0.0;
+    const int jl = lane < Nn ? lane : 0;
+    if (FAM == FAM_HORSESHOE) {
+      // Tests/horseShoePrior.stan:30-32 in the exponent: lambda_j tau =
+      // r1_l sqrt(r2_l) r1_g sqrt(r2_g) = exp(u1_l + u2_l/2 + u1_g + u2_g/2)
+      const double a1 = qs[5 + Nn + jl], a2 = qs[5 + 2 * Nn + jl];
+      const double g1 = qs[3 + Nn], g2 = qs[4 + Nn];
+      u = qs[3 + jl];
+      hl = exp(fma(0.5, a2, a1) + fma(0.5, g2, g1));
+    } else {
+      u = qs[3 + jl];
+    }
+#pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
-      qs[k] = q.a[s];
-      qe[k] = (k < Pr().D && is_log(k)) ? exp(q.a[s]) : q.a[s];
+      qe[k] = (k < D && is_log(k)) ? exp(q.a[s]) : q.a[s];
     }
-    wave_fence();
-    long long ts = stamp0();
+    if (lane < 3) MP[lane] = exp(q.a[0]);
+    yv = (FAM == FAM_HORSESHOE) ? u * hl : u;
+    if (lane >= Nn) yv = hl = 0.0;
     if (lane < NNP) {
-      double yv = 0.0, hl = 0.0;
-      if (lane < Nn) {
-        if (FAM == FAM_HORSESHOE) {
-          // Tests/horseShoePrior.stan:30-32
-          hl = qe[5 + Nn + lane] * sqrt(qe[5 + 2 * Nn + lane]) * (qe[3 + Nn] * sqrt(qe[4 + Nn]));
-          yv = qs[3 + lane] * hl;
-        } else {
-          yv = qs[3 + lane];
-        }
-      }
       AUX[lane] = yv;
       AUX[32 + lane] = hl;
-      if (Pr().mode != MODE_POLY) MP[4 + lane] = yv;
+      if (!poly) MP[4 + lane] = yv;
     }
-    if (lane < 3) MP[lane] = qe[lane];
-    if (Pr().mode == MODE_POLY) {  // c_l = b_l (K^-1 yGP)_l ; K^-1 padded to NNP x NNP
+    if (poly) {  // c_l = b_l (K^-1 yGP)_l ; K^-1 padded to NNP x NNP
       wave_fence();
-      sub(4, ts);
       if (lane < NNP) {
-        double c = 0.0;
+        double c0 = 0.0, c1 = 0.0;   // two chains of FMAs: half the dependent latency
 #pragma unroll
-        for (int k = 0; k < NNP; ++k) c = fma(Kinv[lane * NNP + k], AUX[k], c);
-        MP[4 + lane] = c * bv[lane];
-      }
-    }
-  }
-
-  // ------------- lp / grad completion from the reduced bin sums --------------
-  __device__ void gather_sums() const {
-    long long ts = stamp0();
-    if (Pr().prior_PD == 0) {
-      double s = 0.0;
-      if (lane < 4 + NNP) {
-#pragma unroll
-        for (int w = 0; w < NGW; ++w) s += part[(slot * NGW + w) * NSLOT + lane];
-      }
-      if (Pr().mode == MODE_POLY) {  // B^T h = K^-1 (b .* M)
-        if (lane >= 4 && lane < 4 + NNP) SUMS[lane] = s * bv[lane - 4];
-        else if (lane < 4) SUMS[lane] = s;
-        wave_fence();
-        sub(2, ts);
-        if (lane < NNP) {
-          double v = 0.0;
-#pragma unroll
-          for (int l = 0; l < NNP; ++l) v = fma(Kinv[lane * NNP + l], SUMS[4 + l], v);
-          s = v;
+        for (int k = 0; k < NNP; k += 2) {
+          c0 = fma(Kinv[lane * NNP + k], AUX[k], c0);
+          c1 = fma(Kinv[lane * NNP + k + 1], AUX[k + 1], c1);
         }
-        wave_fence();
-        sub(3, ts);
-        if (lane < NNP) SUMS[4 + lane] = s;
-      } else if (lane < 4 + NNP) {
-        SUMS[lane] = s;
+        MP[4 + lane] = (c0 + c1) * bv[lane];
       }
     }
-    wave_fence();
   }
 
   // The lp / grad completion is split so that everything depending only on the
@@ -665,7 +643,7 @@ struct Chain {
   // off the critical path), and only a few FMAs per lane remain once the bin
   // sums arrive (lik_part):
   //   grad_k = PG_k + CA_k * S[sidx(k)] + CB_k * famsum,   lp = pr_lp - 0.5 S0 pr_is2
-  // with S = SUMS after gather_sums and famsum = sum_j FW_j S[4+j] (horseshoe).
+  // with S = the bin sums after finish_grad's transform and famsum = sum_j FW_j S[4+j].
   __device__ __forceinline__ int sidx(int k) const {   // which bin sum lane k's gradient needs
     const int D = Pr().D, Nn = Pr().Nn;
     if (k < 3) return 1 + k;
@@ -731,27 +709,22 @@ struct Chain {
           gk = -ls * sg - 2.0 * ls * qk;
           ck = gyf;
           lpc += -ls * fabs(qk) - ls * qk * qk;
-        } else {  // horseshoe (Tests/horseShoePrior.stan:25-43)
-          const double nu = Pr().nu, ek = qe[k];
-          if (k < 3 + Nn) {
-            gk = -qk;
-            ck = gyf * AUX[32 + (k - 3)];
-            lpc += -0.5 * qk * qk;
-          } else if (k == 3 + Nn) {
-            gk = 1.0 - ek * ek;
-            lpc += -0.5 * ek * ek + qk;
-          } else if (k == 4 + Nn) {
-            gk = 0.5 / ek - 0.5;
-            lpc += -1.5 * qk - 0.5 / ek + qk;
-          } else if (k < 5 + 2 * Nn) {
-            gk = 1.0 - ek * ek;
-            ck = gyf * AUX[k - 5 - Nn];
-            lpc += -0.5 * ek * ek + qk;
-          } else {
-            gk = -0.5 * nu + 0.5 * nu / ek;
-            ck = 0.5 * gyf * AUX[k - 5 - 2 * Nn];
-            lpc += -(0.5 * nu + 1.0) * qk - 0.5 * nu / ek + qk;
-          }
+        } else {  // horseshoe (Tests/horseShoePrior.stan:25-43), straight-line over lanes:
+          //   z_j      : grad -q              lp -q^2/2
+          //   r1 (g, l): grad 1 - e^2         lp -e^2/2 + q          (half-normal + log-Jacobian)
+          //   r2 (g, l): grad c (1/e - 1)     lp -c (q + 1/e)        (InvGamma(c, c) + log-Jacobian,
+          //                                                         c = 1/2 global, nu/2 local)
+          const double ek = qe[k];
+          const bool tz = k < 3 + Nn;
+          const bool r1l = k >= 5 + Nn && k < 5 + 2 * Nn, r2l = k >= 5 + 2 * Nn;
+          const bool tr1 = k == 3 + Nn || r1l;
+          const double cc = (k == 4 + Nn) ? 0.5 : 0.5 * Pr().nu;
+          const double e2 = ek * ek, ie = 1.0 / ek;
+          gk = tz ? -qk : tr1 ? 1.0 - e2 : cc * ie - cc;
+          lpc += tz ? -0.5 * qk * qk : tr1 ? fma(-0.5, e2, qk) : -cc * (qk + ie);
+          const int ai = tz ? 32 + (k - 3) : r1l ? k - 5 - Nn : r2l ? k - 5 - 2 * Nn : 0;
+          const double aw = (tz || r1l) ? 1.0 : r2l ? 0.5 : 0.0;
+          ck = aw * gyf * AUX[ai];
         }
       }
       pg.a[s] = gk;
@@ -766,35 +739,59 @@ struct Chain {
     }
   }
 
-  // After the sweep: reduce the 8 waves' partial sums (gather_sums) and complete
-  // lp / grad from what prior_part left in LDS.  s0 = sum of squared residuals.
+  // After the sweep: reduce the 8 waves' partial sums and complete lp / grad from
+  // what prior_part left in LDS.  s0 = sum of squared residuals.  Two LDS round
+  // trips: bin sums out (-> the K^-1 transform), transformed sums out (-> every
+  // parameter lane); famsum is reduced straight from the transform's lanes.
   __device__ double finish_grad(V& g, double& s0) const {
-    gather_sums();
-    long long ts = stamp0();
     const int Nn = Pr().Nn, D = Pr().D;
-    constexpr int fam = FAM;
-    const bool lik = (Pr().prior_PD == 0);
-    const double S0 = lik ? SUMS[0] : 0.0;
-    double famsum = 0.0;
-    if (fam == FAM_HORSESHOE && lik)
-      famsum = wave_sum(lane < Nn ? AUX[64 + lane] * SUMS[4 + lane] : 0.0);
-    sub(6, ts);
-    const V pg = ld(V_PG), ca = ld(V_CA);
+    const bool lik = (Pr().prior_PD == 0), poly = Pr().mode == MODE_POLY;
+    const V pg = ld(V_PG), ca = ld(V_CA);   // issued up front, used last
+    const double pr_lp = Sp->pr_lp, pr_is2 = Sp->pr_is2;
+    const double fw = (FAM == FAM_HORSESHOE && lane < Nn) ? AUX[64 + lane] : 0.0;
+    double famsum = 0.0, S0 = 0.0;
+    if (lik) {
+      double sl = 0.0;
+      if (lane < 4 + NNP) {
+#pragma unroll
+        for (int w = 0; w < NGW; ++w) sl += part[(slot * NGW + w) * NSLOT + lane];
+        if (poly && lane >= 4) sl *= bv[lane - 4];   // b .* M  (B^T h = K^-1 (b .* M))
+        SUMS[lane] = sl;
+      }
+      S0 = rl(sl, 0);
+      wave_fence();
+      double v = 0.0;
+      if (lane < NNP) {
+        if (poly) {
+          double v1 = 0.0;
+#pragma unroll
+          for (int m = 0; m < NNP; m += 2) {
+            v = fma(Kinv[lane * NNP + m], SUMS[4 + m], v);
+            v1 = fma(Kinv[lane * NNP + m + 1], SUMS[4 + m + 1], v1);
+          }
+          v += v1;
+          SUMS[4 + lane] = v;   // every lane's reads above precede this store
+        } else {
+          v = SUMS[4 + lane];
+        }
+      }
+      if (FAM == FAM_HORSESHOE) famsum = wave_sum(lane < Nn ? fw * v : 0.0);
+      wave_fence();
+    }
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
       double gk = pg.a[s];
       if (lik && k < D) {
         gk = fma(ca.a[s], SUMS[sidx(k)], gk);
-        if (fam == FAM_HORSESHOE && (k == 3 + Nn || k == 4 + Nn))
+        if (FAM == FAM_HORSESHOE && (k == 3 + Nn || k == 4 + Nn))
           gk = fma(k == 3 + Nn ? 1.0 : 0.5, famsum, gk);
       }
       g.a[s] = gk;
     }
     s0 = lik ? S0 : NAN;
-    double lp = fma(-0.5 * S0, Sp->pr_is2, Sp->pr_lp);
+    double lp = fma(-0.5 * S0, pr_is2, pr_lp);
     if ((lik && !(S0 <= DBL_MAX)) || !(fabs(lp) <= DBL_MAX)) lp = -INFINITY;
-    sub(7, ts);
     return lp;
   }
 
@@ -1444,7 +1441,7 @@ constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded,
 // the next position.  Chains cycle independently (no barrier after start-up),
 // so the sampler latency of one chain hides behind the sweeps of the others.
 template <class R, int BPT, int NNP, int PPL, int MODE, int FAM>
-__global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict__ Pg) {
+__global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict__ Pg) {
   KPc& P = *(KPc*)Pg;   // device-resident parameter block: uniform s_load reads
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const Lds<PPL> L{(AS_LDS char*)smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
@@ -1454,18 +1451,28 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
   const int nct = min(P.G, P.chains - c0);
   __shared__ unsigned long long ring[RINGN];
   __shared__ int q_reserve, n_active, grad_cnt[GMAX];
+  __shared__ long long done_t[GMAX];   // profiling build: when the 8th wave finished chain c
+  __shared__ long long start_min[GMAX], start_max[GMAX];
 
   load_kinv<PPL, NNP>(P, L, tid);
   if (tid == 0) {
     q_reserve = 0;
     n_active = nct;
   }
-  if (tid < GMAX) grad_cnt[tid] = 0;
+  if (tid < GMAX) {
+    grad_cnt[tid] = 0;
+    done_t[tid] = 0;
+    start_min[tid] = 0x7FFFFFFFFFFFFFFFLL;
+    start_max[tid] = 0;
+  }
   if (tid < RINGN) ring[tid] = ~0ULL;
   __syncthreads();
 
   const bool stamp = kProfile && (P.stamps != nullptr) && lane == 0 && (wave == 0 || wave == NGW);
-  long long t_busy = 0, n_items = 0, t_wait = 0;
+  const bool wstamp = kProfile && (P.stamps != nullptr) && lane == 0 && wave < NGW;
+  long long t_wbusy = 0;
+  long long t_busy = 0, n_items = 0, t_wait = 0, t_enq = 0, t_sweep = 0, t_notice = 0;
+  long long t_st0 = 0, t_st1 = 0;
   long long t_begin = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
   if (wave < NGW) {  // ------------------------- gradient waves
     Bins<R, BPT, NNP, MODE> bins;
@@ -1487,11 +1494,22 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
       if (stop) break;
       const int c = (int)(e & 0xFF);
       const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+      const long long s0w = wstamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+      if (kProfile && lane == 0) {   // sweep start spread over the 8 waves
+        const unsigned long long t = (unsigned long long)__builtin_amdgcn_s_memtime();
+        atomicMin((unsigned long long*)&start_min[c], t);
+        atomicMax((unsigned long long*)&start_max[c], t);
+      }
       if (P.prior_PD == 0)
         gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1, tid,
                                          lane, wave);
       wave_fence();   // this wave's PART writes are complete
-      if (lane == 0) atomicAdd(&grad_cnt[c], 1);
+      if (wstamp) t_wbusy += (long long)__builtin_amdgcn_s_memtime() - s0w;
+      if (lane == 0) {
+        if (kProfile)   // latest finisher's time; LDS ops of a wave complete in order
+          atomicMax((unsigned long long*)&done_t[c], (unsigned long long)__builtin_amdgcn_s_memtime());
+        atomicAdd(&grad_cnt[c], 1);
+      }
       if (stamp) {
         t_busy += (long long)__builtin_amdgcn_s_memtime() - s0;
         ++n_items;
@@ -1520,7 +1538,16 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
             if (++spins > SPIN_LIMIT) break;
             __builtin_amdgcn_s_sleep(1);
           }
-          if (stamp) t_wait += (long long)__builtin_amdgcn_s_memtime() - w0;
+          if (stamp) {
+            const long long t1 = (long long)__builtin_amdgcn_s_memtime();
+            t_wait += t1 - w0;
+            t_sweep += done_t[c] - t_enq;            // enqueue -> 8th gradient wave done
+            t_st0 += start_min[c] - t_enq;           // enqueue -> first wave starts
+            t_st1 += start_max[c] - t_enq;           // enqueue -> last wave starts
+            start_min[c] = 0x7FFFFFFFFFFFFFFFLL;
+            start_max[c] = 0;
+            t_notice += t1 - (done_t[c] > w0 ? done_t[c] : w0);
+          }
           if (spins > SPIN_LIMIT) {
             ch.Sp->status = ERR_TIMEOUT;
             a = Ch::A_FINISH;
@@ -1545,6 +1572,7 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
           __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
                            __ATOMIC_RELAXED);
         }
+        if (stamp) t_enq = (long long)__builtin_amdgcn_s_memtime();
         ++epoch;
         // position-only work (prior terms, next merges' uniforms) overlaps the sweep
         a = Ch::A_PRIOR;
@@ -1554,6 +1582,7 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
       if (lane == 0) atomicSub(&n_active, 1);
     }
   }
+  if (wstamp) ((AS_GLB long long*)P.stamps)[(size_t)blockIdx.x * NSTAMP + 56 + wave] = t_wbusy;
   if (stamp) {
     AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)blockIdx.x * NSTAMP;
     if (wave == 0) {
@@ -1563,18 +1592,22 @@ __global__ void __launch_bounds__(TPB, 3) nuts_kernel(const KParams* __restrict_
     } else {
       o[2] = t_busy;
       o[40] = t_wait;
+      o[42] = t_sweep;
+      o[43] = t_notice;
+      o[44] = t_st0;
+      o[45] = t_st1;
       o[41] = n_items;
       for (int k = 0; k < 18; ++k) {
         o[4 + k] = L.cs(0).prof[0][k];
         o[22 + k] = L.cs(0).prof[1][k];
       }
-      for (int k = 0; k < 12; ++k) o[48 + k] = L.cs(0).prof[0][20 + k];
+      for (int k = 0; k < 8; ++k) o[48 + k] = L.cs(0).prof[0][20 + k];
     }
   }
 }
 
 template <class R, int BPT, int NNP, int PPL, int MODE, int FAM>
-__global__ void __launch_bounds__(TPB, 3) logp_kernel(const KParams* __restrict__ Pg) {
+__global__ void __launch_bounds__(TPB, 2) logp_kernel(const KParams* __restrict__ Pg) {
   KPc& P = *(KPc*)Pg;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const Lds<PPL> L{(AS_LDS char*)smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
@@ -1668,6 +1701,9 @@ static hipError_t launch_m(bool logp, int bpt, const KParams& P, const KParams* 
     case 1: return launch_t<R, 1, NNP, PPL, MODE>(logp, P, dP, tiles, st);
     case 2: return launch_t<R, 2, NNP, PPL, MODE>(logp, P, dP, tiles, st);
     case 4: return launch_t<R, 4, NNP, PPL, MODE>(logp, P, dP, tiles, st);
+    case 8:
+      if constexpr (MODE == MODE_POLY) return launch_t<R, 8, NNP, PPL, MODE>(logp, P, dP, tiles, st);
+      return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
@@ -1687,7 +1723,7 @@ hipError_t FITOCT_CAT(launch_family_, FITOCT_FAMILY)(bool logp, bool mixed, int 
                                                      const KParams& P, const KParams* dP,
                                                      int tiles, hipStream_t st) {
 #ifdef FITOCT_ONE_VARIANT
-  return launch_t<double, 4, 16, 1, MODE_POLY>(logp, P, dP, tiles, st);
+  return launch_t<double, 8, 16, 1, MODE_POLY>(logp, P, dP, tiles, st);
 #else
   if (nnp == 16) return launch_n<16, 1>(logp, mixed, bpt, P, dP, tiles, st);
   return launch_n<24, 2>(logp, mixed, bpt, P, dP, tiles, st);

@@ -210,14 +210,17 @@ static double logp_grad(const model* m, const double* q, double* g, double* sumr
   const double th[3] = {exp(q[0]), exp(q[1]), exp(q[2])};
   const double usig = q[D - 1], sig = exp(usig);
   double tau = 0.0, lam_s = 0.0;
+  /* horseshoe (Tests/horseShoePrior.stan:30-32): lam[k] holds lambda_k * tau =
+   * r1_l sqrt(r2_l) r1_g sqrt(r2_g), evaluated in the exponent as
+   * exp(u1_l + u2_l/2 + u1_g + u2_g/2) -- the same expression as the HIP sampler */
   for (int k = 0; k < Nn; ++k) {
     if (fam == 2) {
-      lam[k] = exp(q[5 + Nn + k]) * sqrt(exp(q[5 + 2 * Nn + k]));
+      lam[k] = exp(fma(0.5, q[5 + 2 * Nn + k], q[5 + Nn + k]) + fma(0.5, q[4 + Nn], q[3 + Nn]));
     }
     gy[k] = 0.0;
   }
-  if (fam == 2) tau = exp(q[3 + Nn]) * sqrt(exp(q[4 + Nn]));
-  for (int k = 0; k < Nn; ++k) ygp[k] = fam == 2 ? q[3 + k] * lam[k] * tau : q[3 + k];
+  if (fam == 2) tau = 1.0; /* folded into lam[] */
+  for (int k = 0; k < Nn; ++k) ygp[k] = fam == 2 ? q[3 + k] * lam[k] : q[3 + k];
   if (fam == 0) lam_s = exp(q[3 + Nn]);
   double lp = 0.0, gth[3] = {0, 0, 0}, gsig = 0.0;
   int bad = 0;
