@@ -258,21 +258,40 @@ template <> __device__ __forceinline__ double rcp_<double>(double x) {
   double e = fma(-x, r, 1.0);
   r = fma(r, e, r);
   e = fma(-x, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-x, r, 1.0);
-  return fma(r, e, r);                          // <= 1 ulp
+  return fma(r, e, r);   // 2 Newton steps: 0 ulp from 1/x over 4M samples (scripts/micro/acc.hip)
 }
 template <> __device__ __forceinline__ float rcp_<float>(float x) {
   return __builtin_amdgcn_rcpf(x);
 }
 template <class R> __device__ __forceinline__ R exp_(R x);
-template <> __device__ __forceinline__ double exp_<double>(double x) { return exp(x); }
+// exp for the sweep: reduction by ln2 (hi/lo), Taylor degree 12 on |r| <= ln2/2,
+// ldexp.  <= 2 ulp from the library exp on [-700, 0] (scripts/micro/acc.hip) and
+// no special-case selects: arguments here are <= 0, underflow ends in 0 via ldexp.
+template <> __device__ __forceinline__ double exp_<double>(double x) {
+  const double n = rint(x * 1.4426950408889634);
+  double r = fma(-n, 6.93147180369123816490e-01, x);
+  r = fma(-n, 1.90821492927058770002e-10, r);
+  double p = 2.08767569878680989792e-09;   // 1/12!
+  p = fma(p, r, 2.50521083854417187751e-08);
+  p = fma(p, r, 2.75573192239858906526e-07);
+  p = fma(p, r, 2.75573192239858906526e-06);
+  p = fma(p, r, 2.48015873015873015873e-05);
+  p = fma(p, r, 1.98412698412698412698e-04);
+  p = fma(p, r, 1.38888888888888888889e-03);
+  p = fma(p, r, 8.33333333333333333333e-03);
+  p = fma(p, r, 4.16666666666666666667e-02);
+  p = fma(p, r, 1.66666666666666666667e-01);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, (int)n);
+}
 template <> __device__ __forceinline__ float exp_<float>(float x) { return __expf(x); }
 
 // Likelihood terms of one bin given its modulation dL (shared by every mode).
 // acc: [0] sum d^2, [1] sum a, [2] sum a e, [3] sum w; returns h (adjoint seed of dL).
-template <class R, class A>
-__device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th3, A (&acc)[NSLOT]) {
+template <class R, class A, int NA>
+__device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th3, A (&acc)[NA]) {
   const R u = R(1) + dL;
   const R L = th3 * u;                                           // decay length theta3*(1+dL)
   const R iL = rcp_<R>(L);
@@ -293,11 +312,11 @@ __device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th
 // MODE_POLY: dL = a P(t) with P = sum_l c_l t^l ; moments M_l += h a t^l
 template <class R, int NNP, class A>
 __device__ __forceinline__ void bin_poly(R cx, R y, R isu, R t, R av, R th1, R th2, R th3,
-                                         const R (&cf)[NNP], A (&acc)[NSLOT]) {
+                                         const R (&cf)[NNP], A (&acc)[4 + NNP]) {
   R P = cf[NNP - 1];
 #pragma unroll
   for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
-  const R h = bin_core<R, A>(av * P, cx, y, isu, th1, th2, th3, acc);
+  const R h = bin_core<R, A, 4 + NNP>(av * P, cx, y, isu, th1, th2, th3, acc);
   R p = h * av;
   acc[4] += (A)p;
 #pragma unroll
@@ -310,11 +329,11 @@ __device__ __forceinline__ void bin_poly(R cx, R y, R isu, R t, R av, R th1, R t
 // MODE_ROWS / MODE_STREAM: dL = B_i . yGP ; (B^T h)_k += B_ik h
 template <class R, int NNP, class A>
 __device__ __forceinline__ void bin_rows(R cx, R y, R isu, const R (&Brow)[NNP], R th1, R th2,
-                                         R th3, const R (&yg)[NNP], A (&acc)[NSLOT]) {
+                                         R th3, const R (&yg)[NNP], A (&acc)[4 + NNP]) {
   R dL = R(0);
 #pragma unroll
   for (int k = 0; k < NNP; ++k) dL = fma(Brow[k], yg[k], dL);
-  const R h = bin_core<R, A>(dL, cx, y, isu, th1, th2, th3, acc);
+  const R h = bin_core<R, A, 4 + NNP>(dL, cx, y, isu, th1, th2, th3, acc);
 #pragma unroll
   for (int k = 0; k < NNP; ++k) acc[4 + k] = fma((A)Brow[k], (A)h, acc[4 + k]);
 }
@@ -350,14 +369,47 @@ __device__ __forceinline__ bool transpose_all_positive8(double (&v)[8], int lane
   return ok == __builtin_amdgcn_read_exec();
 }
 
-__device__ __forceinline__ double transpose_reduce32(double (&v)[NSLOT], int lane) {
+// The transposed butterfly for any NV <= 32 values: halves the live values per
+// step (ceil), a missing partner counts as zero.  Returns the lane's total and,
+// in idx, which value it is (-1: a padding lane).
+template <int H, int N, int CTRL, int NV>
+__device__ __forceinline__ void tr_dpp_n(double (&v)[NV], bool up) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) v[i] = swap32_add(v[i], v[i + 16]);   // lanes >= 32 keep [16,32)
+  for (int i = 0; i < H; ++i) {
+    double send, keep;
+    if (i + H < N) {
+      send = up ? v[i] : v[i + H];
+      keep = up ? v[i + H] : v[i];
+    } else {
+      send = up ? v[i] : 0.0;
+      keep = up ? 0.0 : v[i];
+    }
+    v[i] = keep + dpp<CTRL>(send);
+  }
+}
+template <int NV>
+__device__ __forceinline__ double transpose_reduce(double (&v)[NV], int lane, int& idx) {
+  constexpr int c1 = (NV + 1) / 2, c2 = (c1 + 1) / 2, c3 = (c2 + 1) / 2, c4 = (c3 + 1) / 2;
+  constexpr int c5 = (c4 + 1) / 2;
+  static_assert(NV <= 32 && c5 == 1, "transpose_reduce: at most 32 values");
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = swap16_add(v[i], v[i + 8]);     // odd rows keep [8,16)
-  tr_dpp<4, DPP_MIRROR>(v, (lane & 8) != 0);
-  tr_dpp<2, DPP_HALF_MIRROR>(v, (lane & 4) != 0);
-  tr_dpp<1, DPP_QREV>(v, (lane & 2) != 0);
+  for (int i = 0; i < c1; ++i) v[i] = swap32_add(v[i], i + c1 < NV ? v[i + c1] : 0.0);
+#pragma unroll
+  for (int i = 0; i < c2; ++i) v[i] = swap16_add(v[i], i + c2 < c1 ? v[i + c2] : 0.0);
+  tr_dpp_n<c3, c2, DPP_MIRROR>(v, (lane & 8) != 0);
+  tr_dpp_n<c4, c3, DPP_HALF_MIRROR>(v, (lane & 4) != 0);
+  tr_dpp_n<c5, c4, DPP_QREV>(v, (lane & 2) != 0);
+  int i = (lane & 2) ? c5 : 0;
+  bool ok = i < c4;
+  i += (lane & 4) ? c4 : 0;
+  ok = ok && i < c3;
+  i += (lane & 8) ? c3 : 0;
+  ok = ok && i < c2;
+  i += (lane & 16) ? c2 : 0;
+  ok = ok && i < c1;
+  i += (lane & 32) ? c1 : 0;
+  ok = ok && i < NV;
+  idx = ok ? i : -1;
   return v[0] + dpp<DPP_XOR1>(v[0]);
 }
 
@@ -433,9 +485,9 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
     R cf[NNP];   // POLY: c_l = b_l (K^-1 yGP)_l ; ROWS: yGP_k
 #pragma unroll
     for (int k = 0; k < NNP; ++k) cf[k] = (R)mp[4 + k];
-    double acc[NSLOT];
+    double acc[4 + NNP];
 #pragma unroll
-    for (int k = 0; k < NSLOT; ++k) acc[k] = 0.0;
+    for (int k = 0; k < 4 + NNP; ++k) acc[k] = 0.0;
     if constexpr (BPT > 0 && MODE == MODE_POLY) {
 #pragma unroll
       for (int b = 0; b < BPT; ++b)
@@ -443,9 +495,9 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                                  bins.row[b][1], th1, th2, th3, cf, acc);
     } else if constexpr (BPT > 0) {
       // the few bins of one lane accumulate in R, the lane totals in f64
-      R racc[NSLOT];
+      R racc[4 + NNP];
 #pragma unroll
-      for (int k = 0; k < NSLOT; ++k) racc[k] = R(0);
+      for (int k = 0; k < 4 + NNP; ++k) racc[k] = R(0);
 #pragma unroll
       for (int b = 0; b < BPT; ++b)
         bin_rows<R, NNP, R>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b], th1, th2, th3, cf,
@@ -469,9 +521,9 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
         }
       }
     }
-    const double r = transpose_reduce32(acc, lane);
-    const int idx = lane >> 1;
-    if (!(lane & 1) && idx < 4 + NNP) part[(c * NGW + wave) * NSLOT + idx] = r;
+    int idx;
+    const double r = transpose_reduce<4 + NNP>(acc, lane, idx);
+    if (!(lane & 1) && idx >= 0) part[(c * NGW + wave) * NSLOT + idx] = r;
   }
 }
 
