@@ -117,12 +117,21 @@ def main():
 
     import torch
     dist = None
+    # FITOCT_BENCH_BACKEND=gloo rehearses the multi-rank path with ranks sharing
+    # GPUs (RCCL refuses two ranks on one device); the driver's runs use nccl.
+    backend = os.environ.get("FITOCT_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    cdev = dev if backend == "nccl" else torch.device("cpu")   # where collectives run
 
     from fitoct_amd import Plan
     from fitoct_amd.api import SamplerConfig  # noqa: F401  (import check)
@@ -148,11 +157,13 @@ def main():
         if key not in bufs:
             bufs[key] = torch.empty(key // 8, dtype=torch.float64, device=dev)
             if world > 1 and rank == 0:
-                bufs["gather"] = [torch.empty_like(bufs[key]) for _ in range(world)]
+                bufs["gather"] = [torch.empty(key // 8, dtype=torch.float64, device=cdev)
+                                  for _ in range(world)]
         buf = bufs[key]
         pl.run(d_draws=buf.data_ptr(), stream=stream.cuda_stream)
-        if world > 1:
-            dist.gather(buf, gather_list=bufs.get("gather") if rank == 0 else None, dst=0)
+        if world > 1:   # one gather of every rank's draws to rank 0 (RCCL over xGMI)
+            src = buf if backend == "nccl" else buf.cpu()
+            dist.gather(src, gather_list=bufs.get("gather") if rank == 0 else None, dst=0)
         return buf
 
     # ---- untimed warmup steps -------------------------------------------------
@@ -175,14 +186,14 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
     outs = [pl.download(with_draws=(i == len(plans) - 1)) for i, pl in enumerate(plans)]
     lf_steps = [o.total_leapfrogs for o in outs]
     if dist is not None:
-        t = torch.tensor(lf_steps, dtype=torch.float64, device=dev)
+        t = torch.tensor(lf_steps, dtype=torch.float64, device=cdev)
         dist.all_reduce(t)
         lf_all = t.cpu().numpy()
     else:
