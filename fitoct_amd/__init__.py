@@ -6,6 +6,7 @@ include/fitoct.h) -> HIP kernels for gfx950.  See DESIGN.md.
 from .api import (ExpGPProblem, Plan, SampleOutput, SamplerConfig, fitExpGP, logp_grad,
                   sample)
 from ._lib import FitOCTError, lib
+from .monoexp import fitMonoExp, printBr
 
 __all__ = ["ExpGPProblem", "SamplerConfig", "Plan", "SampleOutput", "fitExpGP", "logp_grad",
-           "sample", "FitOCTError", "lib"]
+           "sample", "FitOCTError", "lib", "fitMonoExp", "printBr"]

@@ -15,7 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfitoct.so")
 
-PRIOR = {"normal": 0, "lasso": 1, "horseshoe": 2}
+PRIOR = {"normal": 0, "lasso": 1, "horseshoe": 2, "monoexp": 3}   # monoexp: FITOCT_MODEL_MONOEXP
 GRID = {"internal": 0, "extremal": 1}
 PREC = {"f64": 0, "mixed": 1}
 

@@ -28,6 +28,7 @@ SOURCES = [
     ("nuts_normal", "nuts_device.hip", "hipcc", _KERNEL + ["-DFITOCT_FAMILY=0"]),
     ("nuts_lasso", "nuts_device.hip", "hipcc", _KERNEL + ["-DFITOCT_FAMILY=1"]),
     ("nuts_horseshoe", "nuts_device.hip", "hipcc", _KERNEL + ["-DFITOCT_FAMILY=2"]),
+    ("nuts_monoexp", "nuts_device.hip", "hipcc", _KERNEL + ["-DFITOCT_FAMILY=3"]),
     ("fitoct_api", "fitoct_api.cpp", "hipcc", [f"--offload-arch={ARCH}", "-O2", "-std=c++17"]),
     ("host_model", "host_model.cpp", "g++", ["-O2", "-std=c++17"]),
 ]

@@ -23,6 +23,8 @@ hipError_t launch_family_1(bool logp, bool mixed, int bpt, int nnp, const KParam
                            const KParams* dP, int tiles, hipStream_t st);
 hipError_t launch_family_2(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
                            const KParams* dP, int tiles, hipStream_t st);
+hipError_t launch_family_3(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
+                           const KParams* dP, int tiles, hipStream_t st);
 // the sampler is compiled per prior family (nuts_device.hip, -DFITOCT_FAMILY)
 inline hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
                          const KParams* dP, int tiles, hipStream_t st) {
@@ -30,6 +32,7 @@ inline hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams&
     case 0: return launch_family_0(logp, mixed, bpt, nnp, P, dP, tiles, st);
     case 1: return launch_family_1(logp, mixed, bpt, nnp, P, dP, tiles, st);
     case 2: return launch_family_2(logp, mixed, bpt, nnp, P, dP, tiles, st);
+    case 3: return launch_family_3(logp, mixed, bpt, nnp, P, dP, tiles, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -71,7 +74,9 @@ int check_problem(const fitoct_problem* p) {
   if (!p) return fail(FITOCT_E_ARG, "problem is NULL");
   if (p->N < 2) return fail(FITOCT_E_ARG, "N must be >= 2");
   if (!p->x || !p->y || !p->uy) return fail(FITOCT_E_ARG, "x, y, uy must be non-NULL");
-  if (p->Nn < 2 || p->Nn > 24) return fail(FITOCT_E_ARG, "Nn must be in [2, 24]");
+  const bool mono = p->prior_type == FITOCT_MODEL_MONOEXP;
+  if (!mono && (p->Nn < 2 || p->Nn > 24)) return fail(FITOCT_E_ARG, "Nn must be in [2, 24]");
+  if (mono && p->prior_PD) return fail(FITOCT_E_ARG, "the mono-exponential model has a flat prior: prior_PD must be 0");
   if (model_dim(p->prior_type, p->Nn) < 0) return fail(FITOCT_E_ARG, "unknown prior_type");
   if (p->data_type != 1 && p->data_type != 2) return fail(FITOCT_E_ARG, "data_type must be 1 or 2");
   for (int i = 0; i < p->N; ++i) {
@@ -252,8 +257,11 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   pl->ppl = (D <= WAVE) ? 1 : 2;
   if (pl->nnp == 16 && pl->ppl == 2) pl->nnp = 24;  // the (24, 2) instantiation covers it
   if (pl->nnp == 24) pl->ppl = 2;
+  const bool mono = p->prior_type == FITOCT_MODEL_MONOEXP;
   std::vector<double> B, xg;
-  if (p->B) {
+  if (mono) {
+    // no GP term: a factorised basis of zeros (dL = 0); Nn = 0 inside the kernel
+  } else if (p->B) {
     B.assign(p->B, p->B + (size_t)p->N * p->Nn);
   } else {
     rc = build_basis(p, B, xg);
@@ -262,7 +270,10 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   // basis mode (see kernel_params.h BasisMode)
   std::vector<double> ta, kinv, bv;
   int mode;
-  if (pl->mixed) {
+  if (mono) {
+    mode = MODE_POLY;
+    ta.assign(2 * (size_t)p->N, 0.0);
+  } else if (pl->mixed) {
     mode = MODE_ROWS;
   } else {
     const bool poly = !p->B && getenv("FITOCT_NO_POLY") == nullptr &&
@@ -295,13 +306,17 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   k.bvec = dk + kinv.size();
   k.N = p->N;
   k.n_pad = n_pad;
-  k.Nn = p->Nn;
+  k.Nn = mono ? 0 : p->Nn;
   k.D = D;
   k.family = p->prior_type;
   k.prior_PD = p->prior_PD ? 1 : 0;
   for (int j = 0; j < 3; ++j) k.theta0[j] = p->theta0[j];
-  rc = invert3(p->Sigma0, k.S0inv);
-  if (rc) return rc;
+  if (mono) {
+    for (int j = 0; j < 9; ++j) k.S0inv[j] = 0.0;
+  } else {
+    rc = invert3(p->Sigma0, k.S0inv);
+    if (rc) return rc;
+  }
   k.lambda_rate_eff = (p->lambda_conv == 0) ? 1.0 / p->lambda_rate : p->lambda_rate;
   k.lambda_scale = p->lambda_scale;
   k.nu = p->nu;

@@ -87,6 +87,7 @@ int model_dim(int prior, int Nn) {
     case FITOCT_PRIOR_NORMAL: return Nn + 5;
     case FITOCT_PRIOR_LASSO: return Nn + 4;
     case FITOCT_PRIOR_HORSESHOE: return 3 * Nn + 6;
+    case FITOCT_MODEL_MONOEXP: return 3;
     default: return -1;
   }
 }

@@ -60,7 +60,7 @@ namespace fitoct {
 #define AS_CST __attribute__((address_space(4)))
 using KPc = const AS_CST KParams;
 
-enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2 };
+enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2, FAM_MONO = 3 };
 
 // Cycle stamps (FITOCT_STAMPS) exist only in a profiling build
 // (FITOCT_PROFILE=1 python -m fitoct_amd.build): the production kernels carry
@@ -711,9 +711,12 @@ struct Chain {
     const AS_LDS double* qs = QS();
     const AS_LDS double* qe = QE();
     const bool lik = (Pr().prior_PD == 0);
+    constexpr bool mono = FAM == FAM_MONO;   // flat theta prior, sigma = 1 (fitMonoExp)
     const double th0 = qe[0], th1 = qe[1], th2 = qe[2];
-    const double usig = qs[D - 1], sig = qe[D - 1], is2 = 1.0 / (sig * sig);
-    const double d0 = th0 - Pr().theta0[0], d1 = th1 - Pr().theta0[1], d2 = th2 - Pr().theta0[2];
+    const double usig = mono ? 0.0 : qs[D - 1], sig = mono ? 1.0 : qe[D - 1];
+    const double is2 = mono ? 1.0 : 1.0 / (sig * sig);
+    const double d0 = mono ? 0.0 : th0 - Pr().theta0[0], d1 = mono ? 0.0 : th1 - Pr().theta0[1],
+                 d2 = mono ? 0.0 : th2 - Pr().theta0[2];
     const AS_CST double* Si = Pr().S0inv;
     const double Sd0 = Si[0] * d0 + Si[1] * d1 + Si[2] * d2;
     const double Sd1 = Si[3] * d0 + Si[4] * d1 + Si[5] * d2;
@@ -724,7 +727,7 @@ struct Chain {
     if (lane == 0) {
       if (lik) lpc += -(double)Pr().N * usig;
       lpc += -0.5 * (d0 * Sd0 + d1 * Sd1 + d2 * Sd2t) + qs[0] + qs[1] + qs[2];
-      lpc += -0.5 * (sig / ss) * (sig / ss) + usig;
+      if (!mono) lpc += -0.5 * (sig / ss) * (sig / ss) + usig;
     }
     double ysum = 0.0;   // normal family: sum yGP^2
     if (fam == FAM_NORMAL) ysum = wave_sum(lane < Nn ? AUX[lane] * AUX[lane] : 0.0);
@@ -741,6 +744,8 @@ struct Chain {
           const double sdk = (k == 0) ? Sd0 : (k == 1) ? Sd1 : Sd2t;
           gk = 1.0 - thk * sdk;
           if (lik) ck = (k == 2) ? th1 * is2 : thk * is2;
+        } else if (mono) {
+          // no other parameter
         } else if (k == D - 1) {
           gk = (lik ? -(double)Pr().N : 0.0) - sig * sig / (ss * ss) + 1.0;
           if (lik) ck = is2;

@@ -1,0 +1,158 @@
+"""``FitOCTLib::fitMonoExp`` and ``printBr`` on the HIP engine.
+
+The reference calls ``fitMonoExp(x, y, uy, dataType)`` (FitOCT.R:95,
+server.R:341-343) and reads ``best.theta`` / ``cor.theta`` (FitOCT.R:96-97),
+``fit$par$m`` / ``fit$par$resid`` (plotMonoExp.R:15-16), ``fit$hessian``
+(server.R:117-126) and the Birge ratio through ``printBr`` (plotMonoExp.R:10,
+FitOCT.R:100).  FitOCTLib itself is not in the reference tree, so the model is
+restated (⚑, include/fitoct.h FITOCT_MODEL_MONOEXP):
+
+    y_i ~ N(theta1 + theta2 exp(-c x_i / theta3), uy_i),  theta > 0, flat prior.
+
+``method='optim'`` is rstan::optimizing: L-BFGS on the log density without the
+Jacobian (the mode in theta), then the Hessian of that function in the
+unconstrained (log theta) space by central differences of the gradient, as
+rstan computes it.  Every log density / gradient is one batched HIP call
+(``fitoct_logp_grad``); the 3-parameter optimiser loop runs on the host.
+``method='sample'`` runs the device NUTS sampler on the same model.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from .api import ExpGPProblem, SamplerConfig, logp_grad, sample
+
+
+def initial_theta(x, y, dataType=2):
+    """A rough (theta1, theta2, theta3) from the data alone (log-linear fit of the
+    decay above its tail level); only the optimiser's / sampler's start."""
+    x = np.asarray(x, float)
+    y = np.asarray(y, float)
+    n = x.size
+    tail = max(3, n // 10)
+    order = np.argsort(x)
+    xs, ys = x[order], y[order]
+    t1 = float(np.median(ys[-tail:]))
+    amp = ys - t1
+    ok = amp > 0.05 * max(float(amp.max()), 1e-12)
+    if ok.sum() >= 3:
+        slope, icpt = np.polyfit(xs[ok], np.log(amp[ok]), 1)
+    else:
+        slope, icpt = -1.0 / max(xs.max() - xs.min(), 1e-12), math.log(max(amp.max(), 1e-12))
+    slope = min(slope, -1e-12)
+    t3 = float(dataType) / -slope
+    t2 = float(math.exp(icpt))
+    return np.array([max(abs(t1), 1e-6), max(t2, 1e-6), max(t3, 1e-6)])
+
+
+def mono_problem(x, y, uy, dataType=2, theta0=None) -> ExpGPProblem:
+    t0 = initial_theta(x, y, dataType) if theta0 is None else np.asarray(theta0, float)
+    return ExpGPProblem(x, y, uy, dataType=dataType, Nn=2, theta0=t0,
+                        Sigma0=np.eye(3), prior_type="monoexp")
+
+
+def decay(x, theta, dataType=2):
+    """``theta1 + theta2 exp(-c x / theta3)`` (ShinyInterface/ui.R:88)."""
+    x = np.asarray(x, float)
+    return theta[0] + theta[1] * np.exp(-float(dataType) * x / theta[2])
+
+
+class OptimFit:
+    """rstan::optimizing-shaped result: ``par``, ``value``, ``hessian``."""
+
+    def __init__(self, par, value, hessian, names, return_code=0, iterations=0):
+        self.par = par
+        self.value = value
+        self.hessian = hessian
+        self.hessian_names = names
+        self.return_code = return_code
+        self.iterations = iterations
+
+    def __repr__(self):
+        return f"OptimFit(theta={self.par['theta']}, value={self.value:.6g})"
+
+
+def _nojac(prob, Q, device):
+    """log density without the log-Jacobian (Stan optimizing) and its gradient."""
+    lp, g, s2 = logp_grad(prob, Q, "f64", device)
+    return lp - Q.sum(axis=1), g - 1.0, s2
+
+
+def fitMonoExp(x, y, uy, dataType=2, method="optim", *, nb_warmup=500, nb_iter=1500,
+               nb_chains=4, seed=None, theta0=None, device=0, hessian_step=1e-5):
+    """Drop-in for ``FitOCTLib::fitMonoExp`` (FitOCT.R:95).  Returns
+    ``dict(fit, method, best.theta, cor.theta)``."""
+    from scipy.optimize import minimize
+
+    prob = mono_problem(x, y, uy, dataType, theta0)
+    if method == "sample":
+        from .stanfit import StanFit
+        if seed is None:
+            seed = int(np.random.SeedSequence().entropy & 0xFFFFFFFF)
+        cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_iter - nb_warmup,
+                            seed=seed, device=device)
+        fit = StanFit.from_output(sample(prob, cfg), prob)
+        th = fit.as_matrix("theta")
+        return {"fit": fit, "method": method, "best.theta": th.mean(axis=0),
+                "cor.theta": np.corrcoef(th.T)}
+    if method != "optim":
+        raise NotImplementedError(f"method={method!r}: 'optim' or 'sample'")
+
+    def f(q):
+        lp, g, _ = _nojac(prob, q[None, :], device)
+        if not np.isfinite(lp[0]):
+            return 1e300, np.zeros(3)
+        return -lp[0], -g[0]
+
+    q0 = np.log(prob.theta0)
+    res = minimize(f, q0, jac=True, method="L-BFGS-B",
+                   options={"maxiter": 2000, "ftol": 1e-15, "gtol": 1e-9})
+    q = res.x
+    # Hessian in the unconstrained space: central differences of the device gradient,
+    # all 6 points in one batched call
+    h = hessian_step
+    Q = np.repeat(q[None, :], 6, axis=0)
+    for j in range(3):
+        Q[2 * j, j] += h
+        Q[2 * j + 1, j] -= h
+    _, G, _ = _nojac(prob, Q, device)
+    H = np.stack([(G[2 * j] - G[2 * j + 1]) / (2 * h) for j in range(3)], axis=1)
+    H = 0.5 * (H + H.T)
+    lp, _, s2 = _nojac(prob, q[None, :], device)
+    theta = np.exp(q)
+    m = decay(x, theta, dataType)
+    resid = (np.asarray(y, float) - m) / np.asarray(uy, float)
+    par = {"theta": theta, "m": m, "resid": resid, "br": float(s2[0]) / len(m)}
+    fit = OptimFit(par, float(lp[0]), H, ["theta.1", "theta.2", "theta.3"],
+                   0 if res.success else 1, int(res.nit))
+    cov_q = np.linalg.inv(-H)
+    cov = cov_q * np.outer(theta, theta)           # delta method back to theta
+    sd = np.sqrt(np.diag(cov))
+    return {"fit": fit, "method": method, "best.theta": theta,
+            "cor.theta": cov / np.outer(sd, sd)}
+
+
+def printBr(fit, N=None, silent=False, prob=0.95):
+    """Birge ratio and its probability interval (FitOCTLib::printBr, used at
+    plotMonoExp.R:10 and FitOCT.R:100).  Under the model, N * br ~ chi2_N, so
+    ``br`` outside the central ``prob`` interval of chi2_N / N raises ``alert``."""
+    from scipy.stats import chi2
+    if isinstance(fit, OptimFit):
+        br = fit.par["br"]
+        N = len(fit.par["resid"])
+    else:
+        draws = fit.extract("br", permuted=True)["br"]
+        br = float(np.mean(draws))
+        if N is None:
+            raise ValueError("N (number of bins) is required for a sampled fit")
+    lo, hi = chi2.ppf([(1 - prob) / 2, (1 + prob) / 2], N) / N
+    alert = None
+    if not (lo <= br <= hi):
+        alert = (f"br = {br:.4g} outside the {100 * prob:g} % probability interval "
+                 f"[{lo:.4g}, {hi:.4g}]")
+    if not silent:
+        print(f"br = {br:.4g}, {100 * prob:g} % probability interval [{lo:.4g}, {hi:.4g}]"
+              + (f"\nAlert: {alert}" if alert else ""))
+    return {"br": br, "interval": (float(lo), float(hi)), "alert": alert}

@@ -49,6 +49,12 @@ typedef enum fitoct_status {
 
 /* yGP hyper-prior families */
 enum { FITOCT_PRIOR_NORMAL = 0, FITOCT_PRIOR_LASSO = 1, FITOCT_PRIOR_HORSESHOE = 2 };
+/* prior_type value selecting the mono-exponential model of FitOCTLib::fitMonoExp
+ * (FitOCT.R:95, server.R:341): y = theta1 + theta2 exp(-c x / theta3), no GP term,
+ * flat prior on theta > 0, sigma fixed at 1 (uy is the noise sd; ⚑ SURVEY §8f row 2).
+ * D = 3; Nn, rho, B, Sigma0 and the hyper-parameters are ignored; theta0 is only
+ * the initialisation centre. */
+enum { FITOCT_MODEL_MONOEXP = 3 };
 /* GP control grid (server.R:627-631) */
 enum { FITOCT_GRID_INTERNAL = 0, FITOCT_GRID_EXTREMAL = 1 };
 /* arithmetic of the per-bin likelihood sweep; reductions and sampler state are f64 always */

@@ -108,7 +108,8 @@ typedef struct {
 } model;
 
 static int dimof(int fam, int Nn) {
-  return fam == 0 ? Nn + 5 : fam == 1 ? Nn + 4 : 3 * Nn + 6;
+  /* fam 3: mono-exponential model (FitOCTLib::fitMonoExp; include/fitoct.h) */
+  return fam == 0 ? Nn + 5 : fam == 1 ? Nn + 4 : fam == 2 ? 3 * Nn + 6 : 3;
 }
 
 static double kern(double d, double rho, int conv) {
@@ -169,18 +170,28 @@ static int basis(const fitoct_problem* p, double* B) {
 static int model_init(model* m, const fitoct_problem* p) {
   memset(m, 0, sizeof *m);
   m->N = p->N;
-  m->Nn = p->Nn;
   m->fam = p->prior_type;
+  m->Nn = m->fam == 3 ? 0 : p->Nn;
   m->D = dimof(p->prior_type, p->Nn);
   m->prior_PD = p->prior_PD;
   m->c = p->data_type;
   m->x = p->x;
   m->y = p->y;
   m->uy = p->uy;
-  m->B = (double*)malloc(sizeof(double) * (size_t)p->N * p->Nn);
-  if (p->B) memcpy(m->B, p->B, sizeof(double) * (size_t)p->N * p->Nn);
-  else if (basis(p, m->B)) return -1;
+  m->B = (double*)malloc(sizeof(double) * (size_t)p->N * (m->Nn > 0 ? m->Nn : 1));
+  if (m->fam == 3) {
+    /* no GP term */
+  } else if (p->B) {
+    memcpy(m->B, p->B, sizeof(double) * (size_t)p->N * p->Nn);
+  } else if (basis(p, m->B)) {
+    return -1;
+  }
   memcpy(m->th0, p->theta0, sizeof m->th0);
+  if (m->fam == 3) { /* flat prior on theta, sigma fixed at 1 */
+    memset(m->Si, 0, sizeof m->Si);
+    m->ss = 1.0;
+    return 0;
+  }
   const double* S = p->Sigma0;
   const double A = S[4] * S[8] - S[5] * S[7], Bc = -(S[3] * S[8] - S[5] * S[6]),
                Cc = S[3] * S[7] - S[4] * S[6];
@@ -208,7 +219,8 @@ static double logp_grad(const model* m, const double* q, double* g, double* sumr
   double* gy = work + Nn;       /* [Nn] */
   double* lam = work + 2 * Nn;  /* [Nn] horseshoe local scales */
   const double th[3] = {exp(q[0]), exp(q[1]), exp(q[2])};
-  const double usig = q[D - 1], sig = exp(usig);
+  const int mono = fam == 3;
+  const double usig = mono ? 0.0 : q[D - 1], sig = mono ? 1.0 : exp(usig);
   double tau = 0.0, lam_s = 0.0;
   /* horseshoe (Tests/horseShoePrior.stan:30-32): lam[k] holds lambda_k * tau =
    * r1_l sqrt(r2_l) r1_g sqrt(r2_g), evaluated in the exponent as
@@ -265,6 +277,10 @@ static double logp_grad(const model* m, const double* q, double* g, double* sumr
     const double sd = m->Si[3 * j] * dt[0] + m->Si[3 * j + 1] * dt[1] + m->Si[3 * j + 2] * dt[2];
     lp += -0.5 * dt[j] * sd + q[j];
     g[j] = th[j] * (gth[j] - sd) + 1.0;
+  }
+  if (mono) {
+    if (!isfinite(lp)) lp = -INFINITY;
+    return lp;
   }
   /* sigma ~ half-normal(0, sigma_scale) */
   lp += -0.5 * (sig / m->ss) * (sig / m->ss) + usig;

@@ -38,8 +38,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 # prior families (same integer codes as include/fitoct.h FITOCT_PRIOR_*)
-NORMAL, LASSO, HORSESHOE = 0, 1, 2
-FAMILIES = {"normal": NORMAL, "lasso": LASSO, "horseshoe": HORSESHOE}
+NORMAL, LASSO, HORSESHOE, MONOEXP = 0, 1, 2, 3
+FAMILIES = {"normal": NORMAL, "lasso": LASSO, "horseshoe": HORSESHOE, "monoexp": MONOEXP}
 
 
 # --------------------------------------------------------------------------
@@ -122,7 +122,10 @@ class Problem:
         self.Sigma0 = np.asarray(self.Sigma0, np.float64).reshape(3, 3)
         if self.rho is None or self.rho == 0:
             self.rho = 1.0 / self.Nn
-        if self.B is None:
+        if self.family == MONOEXP:          # no GP term (FitOCTLib::fitMonoExp)
+            self.B = np.zeros((self.x.size, 0))
+            self.xGP = np.zeros(0)
+        elif self.B is None:
             self.B, self.xGP = gp_basis(self.x, self.Nn, self.grid_type, self.rho,
                                         self.kernel_conv, self.nugget)
 
@@ -137,11 +140,13 @@ class Problem:
 
 def dim(family: int, Nn: int) -> int:
     """Unconstrained dimension (SURVEY §8 shape symbols)."""
-    return {NORMAL: Nn + 5, LASSO: Nn + 4, HORSESHOE: 3 * Nn + 6}[family]
+    return {NORMAL: Nn + 5, LASSO: Nn + 4, HORSESHOE: 3 * Nn + 6, MONOEXP: 3}[family]
 
 
 def param_names(family: int, Nn: int):
     th = ["theta[1]", "theta[2]", "theta[3]"]
+    if family == MONOEXP:
+        return th
     if family == NORMAL:
         return th + [f"yGP[{k+1}]" for k in range(Nn)] + ["lambda", "sigma"]
     if family == LASSO:
@@ -156,6 +161,8 @@ def constrain(q: np.ndarray, family: int, Nn: int) -> np.ndarray:
     q = np.asarray(q, np.float64)
     c = q.copy()
     c[..., 0:3] = np.exp(q[..., 0:3])
+    if family == MONOEXP:
+        return c
     if family == NORMAL:
         c[..., 3 + Nn:] = np.exp(q[..., 3 + Nn:])
     elif family == LASSO:
@@ -194,7 +201,13 @@ def logp_grad(q, prob: Problem):
     assert q.shape == (D,)
     g = np.zeros(D)
     th = np.exp(q[0:3])
-    if fam == HORSESHOE:
+    if fam == MONOEXP:
+        # FitOCTLib::fitMonoExp (⚑ SURVEY §8f row 2): no GP term, flat prior on
+        # theta > 0, sigma fixed at 1 (uy is the noise sd)
+        Nn = 0
+        ygp = np.zeros(0)
+        sigma = 1.0
+    elif fam == HORSESHOE:
         sigma = math.exp(q[D - 1])
         qc = constrain(q, fam, Nn)
         ygp, tau, lam = horseshoe_ygp(qc, Nn)
@@ -237,6 +250,10 @@ def logp_grad(q, prob: Problem):
             gy = th[1] * th[2] * (prob.B.T @ (w / L))       # dlp/dyGP = B^T (dlp/ddL)
             gsig = (float(r @ r) - prob.N) / sigma
 
+    if fam == MONOEXP:
+        g[0:3] = gth * th + 1.0                             # flat prior + log-Jacobian
+        lp += float(q[0:3].sum())
+        return (lp if math.isfinite(lp) else -math.inf), g, sumr2
     # ---- theta ~ multi_normal(theta0, Sigma0)   FitOCT.R:116-117 -------------
     S = np.linalg.inv(prob.Sigma0)
     dth = th - prob.theta0

@@ -40,12 +40,15 @@ LOGP_CASES = {
     "lasso_n97": ("lasso", 97, 8, "internal", 0, 0, 0, 2, "sincExp2"),
     "horseshoe_n128": ("horseshoe", 128, 10, "extremal", 0, 0, 0, 2, "sincExp3"),
     "horseshoe_n481": ("horseshoe", 481, 15, "extremal", 0, 0, 0, 2, "sincExp"),
+    # FitOCTLib::fitMonoExp model (config 1 shape: one synthData.R decay, N=256)
+    "monoexp_n256": ("monoexp", 256, 2, "extremal", 0, 0, 0, 2, "monoExp"),
 }
 
 DRAW_CASES = {
     # name: (family, N, Nn, chains, warmup, samples, seed, max_treedepth)
     "normal_n64": ("normal", 64, 6, 4, 60, 40, 2024, 6),
     "horseshoe_n64": ("horseshoe", 64, 4, 4, 60, 40, 99, 6),
+    "monoexp_n256": ("monoexp", 256, 2, 4, 60, 40, 5, 6),
 }
 
 PHILOX_KAT = [
@@ -63,6 +66,9 @@ def sample_q(fam: int, Nn: int, theta0, rng, n=4):
     for j in range(n):
         q = np.zeros(D)
         q[0:3] = np.log(theta0) + 0.03 * rng.standard_normal(3)
+        if fam == M.MONOEXP:
+            Q[j] = q
+            continue
         if fam == M.HORSESHOE:
             q[3:3 + Nn] = rng.standard_normal(Nn)
             q[3 + Nn:5 + 3 * Nn] = -1.0 + 0.5 * rng.standard_normal(2 + 2 * Nn)

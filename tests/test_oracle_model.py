@@ -60,7 +60,8 @@ def test_gradient_matches_finite_differences(path):
 def test_c_oracle_matches_numpy(path, oracle_c):
     fx = load_golden(path)
     prob, _ = problems_from_fixture(fx)
-    np.testing.assert_allclose(oracle_c.basis(prob), fx["B"], rtol=0, atol=1e-11)
+    if fx["meta"]["family"] != "monoexp":   # no GP basis in the mono-exponential model
+        np.testing.assert_allclose(oracle_c.basis(prob), fx["B"], rtol=0, atol=1e-11)
     lp, g, s2 = oracle_c.logp_grad(prob, fx["q"])
     np.testing.assert_allclose(lp, fx["lp"], rtol=1e-12, atol=1e-9)
     np.testing.assert_allclose(g, fx["grad"], rtol=1e-10, atol=1e-8)
