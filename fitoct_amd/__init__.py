@@ -7,6 +7,8 @@ from .api import (ExpGPProblem, Plan, SampleOutput, SamplerConfig, fitExpGP, log
                   sample)
 from ._lib import FitOCTError, lib
 from .monoexp import fitMonoExp, printBr
+from .optim_vb import Evaluator, OptimFit, optimizing, vb
 
 __all__ = ["ExpGPProblem", "SamplerConfig", "Plan", "SampleOutput", "fitExpGP", "logp_grad",
-           "sample", "FitOCTError", "lib", "fitMonoExp", "printBr"]
+           "sample", "FitOCTError", "lib", "fitMonoExp", "printBr",
+           "Evaluator", "OptimFit", "optimizing", "vb"]

@@ -71,6 +71,45 @@ class PlanInfo(C.Structure):
     ]
 
 
+class OptimConfig(C.Structure):
+    _fields_ = [
+        ("iter", C.c_int32), ("history", C.c_int32), ("init_alpha", C.c_double),
+        ("tol_obj", C.c_double), ("tol_rel_obj", C.c_double), ("tol_grad", C.c_double),
+        ("tol_rel_grad", C.c_double), ("tol_param", C.c_double), ("hessian", C.c_int32),
+        ("jacobian", C.c_int32), ("hessian_step", C.c_double), ("precision", C.c_int32),
+        ("device", C.c_int32),
+    ]
+
+
+class OptimResult(C.Structure):
+    _fields_ = [
+        ("par", _dp), ("hessian", _dp), ("value", C.c_double), ("sumr2", C.c_double),
+        ("iterations", C.c_int32), ("n_evals", C.c_int32), ("termination", C.c_int32),
+        ("return_code", C.c_int32),
+    ]
+
+
+class VbConfig(C.Structure):
+    _fields_ = [
+        ("iter", C.c_int32), ("grad_samples", C.c_int32), ("elbo_samples", C.c_int32),
+        ("eval_elbo", C.c_int32), ("eta", C.c_double), ("adapt_engaged", C.c_int32),
+        ("adapt_iter", C.c_int32), ("tol_rel_obj", C.c_double), ("output_samples", C.c_int32),
+        ("pad_", C.c_int32), ("seed", C.c_uint64), ("precision", C.c_int32), ("device", C.c_int32),
+    ]
+
+
+class VbResult(C.Structure):
+    _fields_ = [
+        ("mu", _dp), ("omega", _dp), ("draws", _dp), ("log_p", _dp), ("log_g", _dp),
+        ("sumr2", _dp), ("eta", C.c_double), ("elbo", C.c_double), ("iterations", C.c_int32),
+        ("converged", C.c_int32), ("n_evals", C.c_int32), ("pad_", C.c_int32),
+    ]
+
+
+TERMINATION = {0: "success", 10: "absolute parameter change", 20: "absolute objective change",
+               21: "relative objective change", 30: "gradient norm", 31: "relative gradient",
+               40: "maximum iterations", -1: "line search failed"}
+
 # every symbol declared in include/fitoct.h: (name, restype, argtypes)
 SIGNATURES = [
     ("fitoct_abi_version", C.c_int32, []),
@@ -92,6 +131,17 @@ SIGNATURES = [
     ("fitoct_plan_run", C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("fitoct_plan_download", C.c_int32, [C.c_void_p, C.POINTER(Result)]),
     ("fitoct_plan_destroy", None, [C.c_void_p]),
+    ("fitoct_evaluator_create", C.c_int32,
+     [C.POINTER(Problem), C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    ("fitoct_evaluator_run", C.c_int32,
+     [C.c_void_p, C.c_int32, _dp, C.c_int32, C.c_int32, _dp, _dp, _dp]),
+    ("fitoct_evaluator_destroy", None, [C.c_void_p]),
+    ("fitoct_constrain", C.c_int32, [C.c_int32, C.c_int32, C.c_int32, _dp, _dp]),
+    ("fitoct_default_optim_config", None, [C.POINTER(OptimConfig)]),
+    ("fitoct_optimize", C.c_int32,
+     [C.POINTER(Problem), C.POINTER(OptimConfig), _dp, C.POINTER(OptimResult)]),
+    ("fitoct_default_vb_config", None, [C.POINTER(VbConfig)]),
+    ("fitoct_vb", C.c_int32, [C.POINTER(Problem), C.POINTER(VbConfig), _dp, C.POINTER(VbResult)]),
     ("fitoct_split_rhat_ess", C.c_int32, [_dp, C.c_int32, C.c_int32, _dp, _dp]),
     ("fitoct_rank_rhat", C.c_int32, [_dp, C.c_int32, C.c_int32, _dp]),
 ]

@@ -262,13 +262,15 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
     ``nb_iter`` counts warmup + sampling iterations, as the callers pass
     ``nb_iter = nb_warmup + nb_sample`` (FitOCT.R:121).  ``rho_scale`` <= 0 means
     ``1/Nn`` (FitOCT.R:119).  Only ``method='sample'`` runs on the GPU; 'optim'
-    and 'vb' are SURVEY §8f rank-3 rows and raise NotImplementedError here.
+    and 'vb' run rstan::optimizing / rstan::vb natively over the same device
+    density (:mod:`fitoct_amd.optim_vb`): ``fit`` is then an ``OptimFit``
+    (``fit$par``, ``fit$hessian``) or a StanFit of ADVI draws.
     Returns ``dict(fit, method, xGP, prior_PD, lasso)``.
     """
     from .stanfit import StanFit
 
-    if method != "sample":
-        raise NotImplementedError(f"method={method!r}: only 'sample' is on the HIP path")
+    if method not in ("sample", "optim", "vb"):
+        raise ValueError(f"method={method!r}: 'sample', 'optim' or 'vb' (FitOCT.R:42)")
     if theta0 is None:
         raise ValueError("theta0 is required (FitOCTLib::estimateExpPrior output)")
     nb_sample = int(nb_iter) - int(nb_warmup)
@@ -280,11 +282,17 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
                         lambda_scale=lambda_scale, nu=nu, prior_PD=prior_PD, **model_switches)
     if seed is None:
         seed = int(np.random.SeedSequence().entropy & 0xFFFFFFFF)
+    _, xGP = prob.basis()
+    if method != "sample":
+        from .optim_vb import optimizing, vb
+        fit = (optimizing(prob, precision=precision, device=device) if method == "optim"
+               else vb(prob, seed=seed, precision=precision, device=device))
+        return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,
+                "lasso": prior_type == "lasso"}
     cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_sample, seed=seed,
                         adapt_delta=adapt_delta, max_treedepth=max_treedepth,
                         precision=precision, device=device)
     out = sample(prob, cfg)
-    _, xGP = prob.basis()
     fit = StanFit.from_output(out, prob)
     return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,
             "lasso": prior_type == "lasso"}

@@ -68,6 +68,17 @@ struct fitoct_plan {
   bool ran = false;
 };
 
+struct fitoct_evaluator {
+  fitoct_plan* pl = nullptr;
+  int capacity = 0, D = 0, cur_n = -1;
+  long long evals = 0;
+  double lp_const = 0.0;
+  double* d_q = nullptr;
+  double* d_out = nullptr;
+  std::vector<char> logmask;
+  std::vector<double> host;
+};
+
 namespace {
 
 int check_problem(const fitoct_problem* p) {
@@ -356,8 +367,6 @@ extern "C" {
 
 int32_t fitoct_abi_version(void) { return FITOCT_ABI_VERSION; }
 
-const char* fitoct_last_error(void) { return g_last_error.c_str(); }
-
 int32_t fitoct_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -438,41 +447,99 @@ int32_t fitoct_build_basis(const fitoct_problem* prob, double* B_out, double* xG
   return FITOCT_OK;
 }
 
+int32_t fitoct_evaluator_create(const fitoct_problem* prob, int32_t capacity, int32_t precision,
+                                int32_t device, fitoct_evaluator** out) {
+  if (!out) return fail(FITOCT_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (capacity < 1) return fail(FITOCT_E_ARG, "capacity must be >= 1");
+  fitoct_evaluator* ev = new fitoct_evaluator();
+  ev->pl = new fitoct_plan();
+  int rc = plan_common(ev->pl, prob, capacity, precision, device, 0);
+  ev->pl->cfg.device = device;
+  auto run = [&]() -> int {
+    if (rc) return rc;
+    const int D = ev->pl->kp.D;
+    ev->capacity = capacity;
+    ev->D = D;
+    ev->lp_const = lp_constant(prob);
+    ev->logmask.resize(D);
+    for (int j = 0; j < D; ++j) ev->logmask[j] = log_transformed(prob->prior_type, prob->Nn, j);
+    HIP_TRY(hipMalloc(&ev->d_q, sizeof(double) * (size_t)capacity * D));
+    HIP_TRY(hipMalloc(&ev->d_out, sizeof(double) * (size_t)capacity * (D + 2)));
+    HIP_TRY(hipMalloc(&ev->pl->d_kp, sizeof(KParams)));
+    KParams& k = ev->pl->kp;
+    k.q_in = ev->d_q;
+    k.grad_out = ev->d_out;
+    return FITOCT_OK;
+  };
+  rc = run();
+  if (rc) {
+    fitoct_evaluator_destroy(ev);
+    return rc;
+  }
+  *out = ev;
+  return FITOCT_OK;
+}
+
+int32_t fitoct_evaluator_run(fitoct_evaluator* ev, int32_t n, const double* q, int32_t jacobian,
+                             int32_t normalised, double* lp_out, double* grad_out,
+                             double* sumr2_out) {
+  if (!ev || !q || !lp_out) return fail(FITOCT_E_ARG, "bad buffers");
+  if (n < 1 || n > ev->capacity) return fail(FITOCT_E_ARG, "n_points must be in [1, capacity]");
+  fitoct_plan* pl = ev->pl;
+  KParams& k = pl->kp;
+  const int D = ev->D;
+  HIP_TRY(hipSetDevice(pl->cfg.device));
+  if (n != ev->cur_n) {  // outputs are laid out for n points: grad[n][D] | lp[n] | sumr2[n]
+    k.chains = n;
+    k.lp_out = ev->d_out + (size_t)n * D;
+    k.s2_out = k.lp_out + n;
+    pl->tiles = (n + k.G - 1) / k.G;
+    HIP_TRY(hipMemcpy(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
+    ev->cur_n = n;
+  }
+  HIP_TRY(hipMemcpy(ev->d_q, q, sizeof(double) * (size_t)n * D, hipMemcpyHostToDevice));
+  HIP_TRY(launch(true, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, 0));
+  // one copy back of grad | lp | sumr2 (contiguous)
+  ev->host.resize((size_t)n * (D + 2));
+  HIP_TRY(hipMemcpy(ev->host.data(), ev->d_out, sizeof(double) * ev->host.size(),
+                    hipMemcpyDeviceToHost));
+  const double* g = ev->host.data();
+  const double* lp = g + (size_t)n * D;
+  for (int i = 0; i < n; ++i) {
+    double v = lp[i];
+    const double* qi = q + (size_t)i * D;
+    if (!jacobian)
+      for (int j = 0; j < D; ++j)
+        if (ev->logmask[j]) v -= qi[j];
+    if (normalised) v += ev->lp_const;
+    lp_out[i] = isfinite(lp[i]) ? v : -INFINITY;
+    if (grad_out)
+      for (int j = 0; j < D; ++j)
+        grad_out[(size_t)i * D + j] = g[(size_t)i * D + j] - ((!jacobian && ev->logmask[j]) ? 1.0 : 0.0);
+    if (sumr2_out) sumr2_out[i] = lp[n + i];
+  }
+  ev->evals += n;
+  return FITOCT_OK;
+}
+
+void fitoct_evaluator_destroy(fitoct_evaluator* ev) {
+  if (!ev) return;
+  (void)hipFree(ev->d_q);
+  (void)hipFree(ev->d_out);
+  free_plan(ev->pl);
+  delete ev;
+}
+
 int32_t fitoct_logp_grad(const fitoct_problem* prob, int32_t n_points, const double* q,
                          double* lp_out, double* grad_out, double* sumr2_out, int32_t precision,
                          int32_t device) {
   if (n_points < 1 || !q || !lp_out || !grad_out) return fail(FITOCT_E_ARG, "bad buffers");
-  fitoct_plan* pl = new fitoct_plan();
-  int rc = plan_common(pl, prob, n_points, precision, device, 0);
-  if (rc) {
-    free_plan(pl);
-    return rc;
-  }
-  KParams k = pl->kp;
-  const int D = k.D;
-  double *d_q = nullptr, *d_out = nullptr;
-  auto run = [&]() -> int {
-    HIP_TRY(hipMalloc(&d_q, sizeof(double) * (size_t)n_points * D));
-    HIP_TRY(hipMalloc(&d_out, sizeof(double) * (size_t)n_points * (D + 2)));
-    HIP_TRY(hipMemcpy(d_q, q, sizeof(double) * (size_t)n_points * D, hipMemcpyHostToDevice));
-    k.q_in = d_q;
-    k.grad_out = d_out;
-    k.lp_out = d_out + (size_t)n_points * D;
-    k.s2_out = k.lp_out + n_points;
-    HIP_TRY(hipMalloc(&pl->d_kp, sizeof(KParams)));
-    HIP_TRY(hipMemcpy(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
-    HIP_TRY(launch(true, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, 0));
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(grad_out, d_out, sizeof(double) * (size_t)n_points * D, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(lp_out, k.lp_out, sizeof(double) * n_points, hipMemcpyDeviceToHost));
-    if (sumr2_out)
-      HIP_TRY(hipMemcpy(sumr2_out, k.s2_out, sizeof(double) * n_points, hipMemcpyDeviceToHost));
-    return FITOCT_OK;
-  };
-  rc = run();
-  (void)hipFree(d_q);
-  (void)hipFree(d_out);
-  free_plan(pl);
+  fitoct_evaluator* ev = nullptr;
+  int rc = fitoct_evaluator_create(prob, n_points, precision, device, &ev);
+  if (rc) return rc;
+  rc = fitoct_evaluator_run(ev, n_points, q, 1, 0, lp_out, grad_out, sumr2_out);
+  fitoct_evaluator_destroy(ev);
   return rc;
 }
 

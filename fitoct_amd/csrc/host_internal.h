@@ -15,5 +15,8 @@ int model_dim(int prior, int Nn);
 std::string column_name(int prior, int Nn, int i);
 int split_rhat_ess(const double* x, int chains, int n, double* rhat, double* ess);
 int rank_rhat(const double* x, int chains, int n, double* out);
+bool log_transformed(int prior, int Nn, int j);
+void constrain(int prior, int Nn, const double* q, double* out);
+double lp_constant(const fitoct_problem* p);
 
 }  // namespace fitoct

@@ -309,4 +309,64 @@ int rank_rhat(const double* x, int chains, int n, double* out) {
   return FITOCT_OK;
 }
 
+// --------------------------------------------------------------------------
+// parameter transforms (Appendix A: positive parameters are log-transformed)
+// --------------------------------------------------------------------------
+bool log_transformed(int prior, int Nn, int j) {
+  const int D = model_dim(prior, Nn);
+  if (j < 3 || j == D - 1) return true;          // theta, sigma (mono: theta only, D = 3)
+  switch (prior) {
+    case FITOCT_PRIOR_NORMAL: return j == 3 + Nn;                 // lambda
+    case FITOCT_PRIOR_HORSESHOE: return j >= 3 + Nn;              // r1/r2 global and local
+    default: return false;                                        // yGP
+  }
+}
+
+void constrain(int prior, int Nn, const double* q, double* out) {
+  const int D = model_dim(prior, Nn);
+  for (int j = 0; j < D; ++j) out[j] = log_transformed(prior, Nn, j) ? exp(q[j]) : q[j];
+}
+
+// Constants dropped from lp by Stan's `~` statements (log_prob<propto=true>)
+// and restored by log_prob<propto=false>: one term per sampling statement of
+// the model contract (Appendix A; horseShoePrior.stan:37-42).
+double lp_constant(const fitoct_problem* p) {
+  const double l2pi = log(2.0 * M_PI);
+  const int Nn = p->Nn;
+  double c = 0.0;
+  if (!p->prior_PD) {
+    c -= 0.5 * p->N * l2pi;
+    for (int i = 0; i < p->N; ++i) c -= log(p->uy[i]);
+  }
+  if (p->prior_type == FITOCT_MODEL_MONOEXP) return c;
+  // theta ~ multi_normal(theta0, Sigma0)
+  const double* S = p->Sigma0;
+  const double det = S[0] * (S[4] * S[8] - S[5] * S[7]) - S[1] * (S[3] * S[8] - S[5] * S[6]) +
+                     S[2] * (S[3] * S[7] - S[4] * S[6]);
+  c += -1.5 * l2pi - 0.5 * log(det);
+  c += -0.5 * l2pi - log(p->sigma_scale);        // sigma ~ normal(0, sigma_scale)
+  if (p->prior_type == FITOCT_PRIOR_NORMAL) {
+    const double rate = (p->lambda_conv == 0) ? 1.0 / p->lambda_rate : p->lambda_rate;
+    c += -0.5 * Nn * l2pi + log(rate);           // yGP ~ normal(0, lambda), lambda ~ exp(rate)
+  } else if (p->prior_type == FITOCT_PRIOR_HORSESHOE) {
+    const double a = 0.5 * p->nu;
+    c += -Nn * l2pi;                                    // z, r1_local ~ normal(0, 1)
+    c += Nn * (a * log(a) - lgamma(a));                 // r2_local ~ inv_gamma(nu/2, nu/2)
+    c += -0.5 * l2pi + 0.5 * log(0.5) - lgamma(0.5);    // r1_global, r2_global
+  }
+  return c;                                      // lasso: `target +=` only, no constant
+}
+
 }  // namespace fitoct
+
+extern "C" int32_t fitoct_constrain(int32_t prior_type, int32_t Nn, int32_t n, const double* q,
+                                    double* out) {
+  using namespace fitoct;
+  const int D = model_dim(prior_type, Nn);
+  if (D < 0) return fail(FITOCT_E_ARG, "unknown prior_type");
+  if (n < 0 || (n > 0 && (!q || !out))) return fail(FITOCT_E_ARG, "bad buffers");
+  for (int i = 0; i < n; ++i) constrain(prior_type, Nn, q + (size_t)i * D, out + (size_t)i * D);
+  return FITOCT_OK;
+}
+
+extern "C" const char* fitoct_last_error(void) { return fitoct::g_last_error.c_str(); }

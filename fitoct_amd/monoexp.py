@@ -9,11 +9,11 @@ restated (⚑, include/fitoct.h FITOCT_MODEL_MONOEXP):
 
     y_i ~ N(theta1 + theta2 exp(-c x_i / theta3), uy_i),  theta > 0, flat prior.
 
-``method='optim'`` is rstan::optimizing: L-BFGS on the log density without the
-Jacobian (the mode in theta), then the Hessian of that function in the
-unconstrained (log theta) space by central differences of the gradient, as
-rstan computes it.  Every log density / gradient is one batched HIP call
-(``fitoct_logp_grad``); the 3-parameter optimiser loop runs on the host.
+``method='optim'`` is rstan::optimizing (:func:`fitoct_amd.optim_vb.optimizing`:
+native L-BFGS on the log density without the Jacobian -- the mode in theta --
+then the Hessian of that function in the unconstrained (log theta) space by
+central differences of the gradient, as rstan's optimHess computes it).  Every
+log density / gradient is a launch of the HIP gradient kernel.
 ``method='sample'`` runs the device NUTS sampler on the same model.
 """
 from __future__ import annotations
@@ -22,7 +22,8 @@ import math
 
 import numpy as np
 
-from .api import ExpGPProblem, SamplerConfig, logp_grad, sample
+from .api import ExpGPProblem, SamplerConfig, sample
+from .optim_vb import OptimFit, optimizing
 
 
 def initial_theta(x, y, dataType=2):
@@ -59,38 +60,15 @@ def decay(x, theta, dataType=2):
     return theta[0] + theta[1] * np.exp(-float(dataType) * x / theta[2])
 
 
-class OptimFit:
-    """rstan::optimizing-shaped result: ``par``, ``value``, ``hessian``."""
-
-    def __init__(self, par, value, hessian, names, return_code=0, iterations=0):
-        self.par = par
-        self.value = value
-        self.hessian = hessian
-        self.hessian_names = names
-        self.return_code = return_code
-        self.iterations = iterations
-
-    def __repr__(self):
-        return f"OptimFit(theta={self.par['theta']}, value={self.value:.6g})"
-
-
-def _nojac(prob, Q, device):
-    """log density without the log-Jacobian (Stan optimizing) and its gradient."""
-    lp, g, s2 = logp_grad(prob, Q, "f64", device)
-    return lp - Q.sum(axis=1), g - 1.0, s2
-
-
 def fitMonoExp(x, y, uy, dataType=2, method="optim", *, nb_warmup=500, nb_iter=1500,
-               nb_chains=4, seed=None, theta0=None, device=0, hessian_step=1e-5):
+               nb_chains=4, seed=None, theta0=None, device=0, hessian_step=1e-3):
     """Drop-in for ``FitOCTLib::fitMonoExp`` (FitOCT.R:95).  Returns
     ``dict(fit, method, best.theta, cor.theta)``."""
-    from scipy.optimize import minimize
-
     prob = mono_problem(x, y, uy, dataType, theta0)
+    if seed is None and method != "optim":
+        seed = int(np.random.SeedSequence().entropy & 0xFFFFFFFF)
     if method == "sample":
         from .stanfit import StanFit
-        if seed is None:
-            seed = int(np.random.SeedSequence().entropy & 0xFFFFFFFF)
         cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_iter - nb_warmup,
                             seed=seed, device=device)
         fit = StanFit.from_output(sample(prob, cfg), prob)
@@ -98,36 +76,13 @@ def fitMonoExp(x, y, uy, dataType=2, method="optim", *, nb_warmup=500, nb_iter=1
         return {"fit": fit, "method": method, "best.theta": th.mean(axis=0),
                 "cor.theta": np.corrcoef(th.T)}
     if method != "optim":
-        raise NotImplementedError(f"method={method!r}: 'optim' or 'sample'")
-
-    def f(q):
-        lp, g, _ = _nojac(prob, q[None, :], device)
-        if not np.isfinite(lp[0]):
-            return 1e300, np.zeros(3)
-        return -lp[0], -g[0]
-
-    q0 = np.log(prob.theta0)
-    res = minimize(f, q0, jac=True, method="L-BFGS-B",
-                   options={"maxiter": 2000, "ftol": 1e-15, "gtol": 1e-9})
-    q = res.x
-    # Hessian in the unconstrained space: central differences of the device gradient,
-    # all 6 points in one batched call
-    h = hessian_step
-    Q = np.repeat(q[None, :], 6, axis=0)
-    for j in range(3):
-        Q[2 * j, j] += h
-        Q[2 * j + 1, j] -= h
-    _, G, _ = _nojac(prob, Q, device)
-    H = np.stack([(G[2 * j] - G[2 * j + 1]) / (2 * h) for j in range(3)], axis=1)
-    H = 0.5 * (H + H.T)
-    lp, _, s2 = _nojac(prob, q[None, :], device)
-    theta = np.exp(q)
+        raise ValueError(f"method={method!r}: 'optim' or 'sample'")
+    fit = optimizing(prob, np.log(prob.theta0), hessian_step=hessian_step, device=device)
+    theta = fit.par["theta"]
     m = decay(x, theta, dataType)
-    resid = (np.asarray(y, float) - m) / np.asarray(uy, float)
-    par = {"theta": theta, "m": m, "resid": resid, "br": float(s2[0]) / len(m)}
-    fit = OptimFit(par, float(lp[0]), H, ["theta.1", "theta.2", "theta.3"],
-                   0 if res.success else 1, int(res.nit))
-    cov_q = np.linalg.inv(-H)
+    fit.par["m"] = m
+    fit.par["resid"] = (np.asarray(y, float) - m) / np.asarray(uy, float)
+    cov_q = np.linalg.inv(-fit.hessian)
     cov = cov_q * np.outer(theta, theta)           # delta method back to theta
     sd = np.sqrt(np.diag(cov))
     return {"fit": fit, "method": method, "best.theta": theta,
@@ -141,7 +96,7 @@ def printBr(fit, N=None, silent=False, prob=0.95):
     from scipy.stats import chi2
     if isinstance(fit, OptimFit):
         br = fit.par["br"]
-        N = len(fit.par["resid"])
+        N = N or fit.N or len(fit.par["resid"])
     else:
         draws = fit.extract("br", permuted=True)["br"]
         br = float(np.mean(draws))

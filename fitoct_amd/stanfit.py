@@ -51,6 +51,33 @@ def rank_rhat(x: np.ndarray) -> float:
     return r.value
 
 
+def add_transformed(draws: np.ndarray, cols: list, prob):
+    """Append the transformed parameters of the horseshoe model (yGP, tau,
+    lambda; Tests/horseShoePrior.stan:25-33) before ``br`` and drop ``br`` for a
+    prior run (plotExpGP.R:42-43).  ``draws[..., len(cols)]`` in column order."""
+    cols = list(cols)
+    if prob.prior_type == "horseshoe":
+        Nn = prob.Nn
+        idx = {c: i for i, c in enumerate(cols)}
+        z = draws[..., [idx[f"z.{k+1}"] for k in range(Nn)]]
+        r1g, r2g = draws[..., idx["r1_global"]], draws[..., idx["r2_global"]]
+        r1l = draws[..., [idx[f"r1_local.{k+1}"] for k in range(Nn)]]
+        r2l = draws[..., [idx[f"r2_local.{k+1}"] for k in range(Nn)]]
+        tau = r1g * np.sqrt(r2g)
+        lam = r1l * np.sqrt(r2l)
+        ygp = z * lam * tau[..., None]
+        br_i = idx["br"]
+        extra = np.concatenate([ygp, tau[..., None], lam], axis=-1)
+        draws = np.concatenate([draws[..., :br_i], extra, draws[..., br_i:]], axis=-1)
+        cols = (cols[:br_i] + [f"yGP.{k+1}" for k in range(Nn)] + ["tau"]
+                + [f"lambda.{k+1}" for k in range(Nn)] + cols[br_i:])
+    if prob.prior_PD:   # plotExpGP.R:42-43: br is not a quantity of the prior run
+        j = cols.index("br")
+        draws = np.delete(draws, j, axis=-1)
+        cols = cols[:j] + cols[j + 1:]
+    return draws, cols
+
+
 class StanFit:
     """Draws of one sampler run: ``draws[chain, iteration, column]``."""
 
@@ -68,26 +95,7 @@ class StanFit:
     @classmethod
     def from_output(cls, out, prob) -> "StanFit":
         """From a :class:`fitoct_amd.api.SampleOutput` (adds transformed parameters)."""
-        draws, cols = out.draws, list(out.columns)
-        if prob.prior_type == "horseshoe":
-            Nn = prob.Nn
-            idx = {c: i for i, c in enumerate(cols)}
-            z = draws[..., [idx[f"z.{k+1}"] for k in range(Nn)]]
-            r1g, r2g = draws[..., idx["r1_global"]], draws[..., idx["r2_global"]]
-            r1l = draws[..., [idx[f"r1_local.{k+1}"] for k in range(Nn)]]
-            r2l = draws[..., [idx[f"r2_local.{k+1}"] for k in range(Nn)]]
-            tau = r1g * np.sqrt(r2g)
-            lam = r1l * np.sqrt(r2l)
-            ygp = z * lam * tau[..., None]
-            br_i = idx["br"]
-            extra = np.concatenate([ygp, tau[..., None], lam], axis=-1)
-            draws = np.concatenate([draws[..., :br_i], extra, draws[..., br_i:]], axis=-1)
-            cols = (cols[:br_i] + [f"yGP.{k+1}" for k in range(Nn)] + ["tau"]
-                    + [f"lambda.{k+1}" for k in range(Nn)] + cols[br_i:])
-        if prob.prior_PD:   # plotExpGP.R:42-43: br is not a quantity of the prior run
-            j = cols.index("br")
-            draws = np.delete(draws, j, axis=-1)
-            cols = cols[:j] + cols[j + 1:]
+        draws, cols = add_transformed(out.draws, list(out.columns), prob)
         return cls(draws, cols, out.warmup_saved, stepsize=out.stepsize,
                    inv_metric=out.inv_metric,
                    meta={"kernel_ms": out.kernel_ms, "total_leapfrogs": out.total_leapfrogs,

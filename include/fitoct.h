@@ -179,6 +179,108 @@ int32_t fitoct_plan_run(fitoct_plan* plan, void* d_draws, void* stream);
 int32_t fitoct_plan_download(fitoct_plan* plan, fitoct_result* res);
 void fitoct_plan_destroy(fitoct_plan* plan);
 
+/* ---- batched density evaluator ------------------------------------------- *
+ * The model of a problem staged once in HBM, evaluated at up to `capacity`
+ * points per call by the same kernel as fitoct_logp_grad (which is a one-shot
+ * evaluator).  Replaces rstan's log_prob / grad_log_prob methods of a stanfit
+ * (used by optimHess inside rstan::optimizing).  `jacobian` = 0 drops the
+ * log-Jacobian of the positivity transforms (Stan optimizing); `normalised` = 1
+ * adds the constants dropped by `~` statements (Stan log_prob<propto=false>). */
+typedef struct fitoct_evaluator fitoct_evaluator;
+int32_t fitoct_evaluator_create(const fitoct_problem* prob, int32_t capacity, int32_t precision,
+                                int32_t device, fitoct_evaluator** out);
+int32_t fitoct_evaluator_run(fitoct_evaluator* ev, int32_t n_points, const double* q,
+                             int32_t jacobian, int32_t normalised, double* lp_out,
+                             double* grad_out /* [n][D] or NULL */, double* sumr2_out);
+void fitoct_evaluator_destroy(fitoct_evaluator* ev);
+/* unconstrained q[n][D] -> constrained parameters in draw-column order (theta,
+ * yGP/z, lambda, sigma, ...: columns 7..7+D-1 of fitoct_column_name) */
+int32_t fitoct_constrain(int32_t prior_type, int32_t Nn, int32_t n_points, const double* q,
+                         double* out);
+
+/* ---- rstan::optimizing (FitOCT.R:42 method='optim'; server.R:156-172) ------ *
+ * L-BFGS on the log density without Jacobian (Stan's defaults below), then the
+ * Hessian on the unconstrained scale by central differences of the gradient
+ * with step `hessian_step` (rstan's optimHess, ndeps = 1e-3), all 2D
+ * displaced points evaluated in one batched launch. */
+typedef struct fitoct_optim_config {
+  int32_t iter;          /* 2000 */
+  int32_t history;       /* 5 */
+  double init_alpha;     /* 1e-3: first line-search step */
+  double tol_obj;        /* 1e-12 */
+  double tol_rel_obj;    /* 1e4  (x machine eps) */
+  double tol_grad;       /* 1e-8 */
+  double tol_rel_grad;   /* 1e7  (x machine eps) */
+  double tol_param;      /* 1e-8 */
+  int32_t hessian;       /* 1: fill res->hessian */
+  int32_t jacobian;      /* 0 (Stan optimizing) */
+  double hessian_step;   /* 1e-3 */
+  int32_t precision;
+  int32_t device;
+} fitoct_optim_config;
+
+/* Stan's BFGS termination codes */
+enum { FITOCT_TERM_SUCCESS = 0, FITOCT_TERM_ABSX = 10, FITOCT_TERM_ABSF = 20,
+       FITOCT_TERM_RELF = 21, FITOCT_TERM_ABSGRAD = 30, FITOCT_TERM_RELGRAD = 31,
+       FITOCT_TERM_MAXIT = 40, FITOCT_TERM_LSFAIL = -1 };
+
+typedef struct fitoct_optim_result {
+  double* par;           /* [D] out: unconstrained optimum (caller-owned) */
+  double* hessian;       /* [D][D] out (NULL = not wanted): Hessian of lp, unconstrained */
+  double value;          /* lp at the optimum (propto=false, jacobian per config) */
+  double sumr2;          /* sum(((y-m)/uy)^2) at the optimum (br = sumr2 / N) */
+  int32_t iterations;
+  int32_t n_evals;       /* density evaluations (points) */
+  int32_t termination;   /* FITOCT_TERM_* */
+  int32_t return_code;   /* 0 = terminated normally (rstan return_code), 70 = error */
+} fitoct_optim_result;
+
+void fitoct_default_optim_config(fitoct_optim_config* cfg);
+/* init_q: [D] unconstrained start (NULL -> theta = theta0, everything else 0) */
+int32_t fitoct_optimize(const fitoct_problem* prob, const fitoct_optim_config* cfg,
+                        const double* init_q, fitoct_optim_result* res);
+
+/* ---- rstan::vb, mean-field ADVI (FitOCT.R:42 method='vb') -------------------- *
+ * Stan's algorithm (Kucukelbir et al. 2017): eta adaptation over
+ * {100, 10, 1, 0.1, 0.01}, adaGrad-style steps, relative-ELBO convergence on a
+ * rolling window.  Random numbers are Philox-addressed by (seed, eta index,
+ * iteration), so the five adaptation runs are evaluated side by side in one
+ * batch and give the same result as Stan's sequential loop would. */
+typedef struct fitoct_vb_config {
+  int32_t iter;            /* 10000 */
+  int32_t grad_samples;    /* 1 */
+  int32_t elbo_samples;    /* 100 */
+  int32_t eval_elbo;       /* 100 */
+  double eta;              /* step size when adapt_engaged = 0 */
+  int32_t adapt_engaged;   /* 1 */
+  int32_t adapt_iter;      /* 50 */
+  double tol_rel_obj;      /* 0.01 */
+  int32_t output_samples;  /* 1000 */
+  int32_t pad_;
+  uint64_t seed;
+  int32_t precision;
+  int32_t device;
+} fitoct_vb_config;
+
+typedef struct fitoct_vb_result {
+  double* mu;              /* [D] out: mean of the approximation (unconstrained) */
+  double* omega;           /* [D] out: log standard deviations */
+  double* draws;           /* [output_samples][D] out: unconstrained draws, or NULL */
+  double* log_p;           /* [output_samples] log density (propto=false, jacobian), or NULL */
+  double* log_g;           /* [output_samples] -0.5 |eta|^2 of each draw, or NULL */
+  double* sumr2;           /* [output_samples] or NULL */
+  double eta;              /* adapted / used step size */
+  double elbo;             /* last ELBO estimate */
+  int32_t iterations;
+  int32_t converged;       /* 1 mean or median relative ELBO change < tol_rel_obj */
+  int32_t n_evals;
+  int32_t pad_;
+} fitoct_vb_result;
+
+void fitoct_default_vb_config(fitoct_vb_config* cfg);
+int32_t fitoct_vb(const fitoct_problem* prob, const fitoct_vb_config* cfg, const double* init_q,
+                  fitoct_vb_result* res);
+
 /* ---- diagnostics (host only) ---------------------------------------------- */
 /* x[chains][n] of one scalar: rstan legacy split-R-hat and n_eff (autocorrelation,
  * Geyer initial monotone sequence), as shown by rstan::summary (server.R:88-104). */

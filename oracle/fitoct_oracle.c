@@ -780,6 +780,19 @@ int oracle_logp_grad(const fitoct_problem* p, int n_points, const double* q, dou
   return 0;
 }
 
+/* standard normals of the ADVI addressing contract (optimize.cpp normals()):
+ * key (seed, stream), counter (it, tag, s, d/2), Box-Muller pairs over d */
+void oracle_normals(uint64_t seed, uint32_t stream, uint32_t tag, uint32_t it, uint32_t s, int D,
+                    double* eta) {
+  const rkey k = chain_key(seed, stream);
+  for (int d = 0; d < D; d += 2) {
+    double n0, n1;
+    normal2(k, it, tag, s, (uint32_t)(d >> 1), &n0, &n1);
+    eta[d] = n0;
+    if (d + 1 < D) eta[d + 1] = n1;
+  }
+}
+
 /* draws: [chains][iters_saved][D + 8] (same columns as libfitoct) */
 int oracle_sample(const fitoct_problem* p, const fitoct_config* cfg, double* draws,
                   double* stepsize, double* inv_metric, long long* leapfrogs, int nthreads) {

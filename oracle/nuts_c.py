@@ -17,10 +17,15 @@ LIB = os.path.join(HERE, "build", "liboracle.so")
 _L = None
 
 
+_BUILT = False
+
+
 def build(force: bool = False) -> str:
-    src = os.path.join(HERE, "fitoct_oracle.c")
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
-        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    """make -C oracle (once per process; make tracks the sources)."""
+    global _BUILT
+    if force or not _BUILT:
+        subprocess.run(["make", "-s", "-C", HERE] + (["-B"] if force else []), check=True)
+        _BUILT = True
     return LIB
 
 
@@ -37,6 +42,8 @@ def lib():
                                     C.POINTER(C.c_longlong), C.c_int]
         L.oracle_philox.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                     C.POINTER(C.c_uint32)]
+        L.oracle_normals.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                     C.c_int, dp]
         _L = L
     return _L
 
@@ -51,6 +58,12 @@ def philox(ctr, key):
     o = (C.c_uint32 * 4)()
     lib().oracle_philox(c, k, o)
     return list(o)
+
+
+def normals(seed, stream, tag, it, s, D):
+    out = np.empty(D)
+    lib().oracle_normals(seed, stream, tag, it, s, D, _dp(out))
+    return out
 
 
 def basis(prob):

@@ -80,8 +80,8 @@ def test_printbr_gate():
 
 def test_argument_contract():
     d = _data(N=64)
-    with pytest.raises(NotImplementedError):
-        fitMonoExp(d["x"], d["y"], d["uy"], method="vb")
+    with pytest.raises(ValueError):
+        fitMonoExp(d["x"], d["y"], d["uy"], method="mcmc")
     prob = mono_problem(d["x"], d["y"], d["uy"])
     assert prob.D == 3 and prob.column_names()[7:] == ["theta.1", "theta.2", "theta.3", "br"]
 

@@ -85,8 +85,8 @@ def test_stan_csv_roundtrip(tmp_path):
 def test_fitexpgp_argument_contract():
     d = synth_decay(32, "sincExp", 1)
     t0, S0 = default_prior()
-    with pytest.raises(NotImplementedError):
-        fitExpGP(d["x"], d["y"], d["uy"], method="optim", theta0=t0, Sigma0=S0)
+    with pytest.raises(ValueError):
+        fitExpGP(d["x"], d["y"], d["uy"], method="mcmc", theta0=t0, Sigma0=S0)
     with pytest.raises(ValueError):
         fitExpGP(d["x"], d["y"], d["uy"], theta0=t0, Sigma0=S0, nb_warmup=100, nb_iter=100)
     with pytest.raises(ValueError):
