@@ -224,6 +224,32 @@ bool build_poly(const fitoct_problem* p, const std::vector<double>& B, int nnp,
   return err <= 1e-10 * std::max(1.0, bmax);
 }
 
+// MODE_POLY with bins in registers: on an arithmetic depth grid the bins
+// tid + b*GT of one lane have t = t_tid * R^b (t_i = exp(u_i dg / s2), u_i linear
+// in i), which lets the sweep form a lane's moments by Horner in R^l
+// (nuts_device.hip moments_geo).  Accepted only if every x_i lies on the line
+// through x_0 and x_{N-1} to 1e-12 of the range and no (R^l)^b can overflow.
+bool geo_ratios(const fitoct_problem* p, int nnp, int bpt, double* R) {
+  const int N = p->N, Nn = p->Nn;
+  if (bpt < 2 || Nn < 2) return false;
+  double xmin = p->x[0], xmax = p->x[0];
+  for (int i = 1; i < N; ++i) {
+    xmin = std::min(xmin, p->x[i]);
+    xmax = std::max(xmax, p->x[i]);
+  }
+  const double range = xmax - xmin, step = (p->x[N - 1] - p->x[0]) / (N - 1);
+  for (int i = 0; i < N; ++i)
+    if (fabs(p->x[i] - (p->x[0] + i * step)) > 1e-12 * range) return false;
+  const double rho = (p->rho > 0.0) ? p->rho : 1.0 / Nn;
+  const double s2 = (p->kernel_conv == 0) ? rho * rho : 0.5 * rho * rho;
+  const double dg = (p->grid_type == FITOCT_GRID_INTERNAL) ? (1.0 - 1.0 / (Nn + 1)) / (Nn - 1)
+                                                           : 1.0 / (Nn - 1);
+  const double logR = GT * (step / range) * dg / s2;
+  if (fabs(logR) * (nnp - 1) * (bpt - 1) > 600.0) return false;
+  for (int l = 0; l < nnp; ++l) R[l] = exp(l * logR);
+  return true;
+}
+
 template <class R>
 void stage(const fitoct_problem* p, const std::vector<double>& B, const std::vector<double>& ta,
            int mode, int n_pad, int nnp, std::vector<char>& out) {
@@ -317,6 +343,8 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   k.bvec = dk + kinv.size();
   k.N = p->N;
   k.n_pad = n_pad;
+  k.geo = (mode == MODE_POLY && !mono && !pl->mixed && getenv("FITOCT_NO_GEO") == nullptr)
+              ? geo_ratios(p, pl->nnp, pl->bpt, k.geo_R) : 0;
   k.Nn = mono ? 0 : p->Nn;
   k.D = D;
   k.family = p->prior_type;

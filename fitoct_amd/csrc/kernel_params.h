@@ -41,6 +41,10 @@ struct KParams {
   const double* Kinv;  // POLY: [Nn][Nn] (K(xGP,xGP) + nugget I)^-1
   const double* bvec;  // POLY: [Nn] b_l
   int N, n_pad, Nn, D, family, prior_PD, mode;
+  // POLY on a uniform depth grid: bin tid + b*GT has t = t_tid * R^b, so a lane's
+  // moments sum_b w_b t_b^l = t_tid^l * sum_b w_b (R^l)^b (Horner in R^l).
+  int geo;                  // 1: geo_R valid (host-verified arithmetic x grid)
+  double geo_R[24];         // R^l, l < NNP
   double theta0[3];
   double S0inv[9];
   double lambda_rate_eff;   // rate of the exponential prior on lambda (normal family)

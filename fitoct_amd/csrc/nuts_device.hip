@@ -326,6 +326,34 @@ __device__ __forceinline__ void bin_poly(R cx, R y, R isu, R t, R av, R th1, R t
   }
 }
 
+// MODE_POLY on a uniform grid: the forward half of bin_poly; returns w = h a,
+// the bin's weight in the moments (accumulated per lane by moments_geo).
+template <class R, int NNP, class A>
+__device__ __forceinline__ R bin_poly_fwd(R cx, R y, R isu, R t, R av, R th1, R th2, R th3,
+                                          const R (&cf)[NNP], A (&acc)[4 + NNP]) {
+  R P = cf[NNP - 1];
+#pragma unroll
+  for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
+  return bin_core<R, A, 4 + NNP>(av * P, cx, y, isu, th1, th2, th3, acc) * av;
+}
+
+// Moments of one lane's BPT bins t_b = t0 R^b:  M_l = t0^l sum_b w_b (R^l)^b.
+// BPT-1 FMAs + 2 multiplies per moment instead of 2 operations per bin and moment.
+template <int BPT, int NNP>
+__device__ __forceinline__ void moments_geo(KPc& P, double t0, const double (&w)[BPT],
+                                            double (&acc)[4 + NNP]) {
+  double pw = 1.0;
+#pragma unroll
+  for (int l = 0; l < NNP; ++l) {
+    const double X = P.geo_R[l];
+    double S = w[BPT - 1];
+#pragma unroll
+    for (int b = BPT - 2; b >= 0; --b) S = fma(S, X, w[b]);
+    acc[4 + l] = pw * S;
+    pw *= t0;
+  }
+}
+
 // MODE_ROWS / MODE_STREAM: dL = B_i . yGP ; (B^T h)_k += B_ik h
 template <class R, int NNP, class A>
 __device__ __forceinline__ void bin_rows(R cx, R y, R isu, const R (&Brow)[NNP], R th1, R th2,
@@ -488,7 +516,21 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
     double acc[4 + NNP];
 #pragma unroll
     for (int k = 0; k < 4 + NNP; ++k) acc[k] = 0.0;
-    if constexpr (BPT > 0 && MODE == MODE_POLY) {
+    if constexpr (BPT > 0 && MODE == MODE_POLY && sizeof(R) == 8) {
+      if (P.geo) {
+        double w[BPT];
+#pragma unroll
+        for (int b = 0; b < BPT; ++b)
+          w[b] = bin_poly_fwd<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
+                                              bins.row[b][1], th1, th2, th3, cf, acc);
+        moments_geo<BPT, NNP>(P, bins.row[0][0], w, acc);
+      } else {
+#pragma unroll
+        for (int b = 0; b < BPT; ++b)
+          bin_poly<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
+                                   bins.row[b][1], th1, th2, th3, cf, acc);
+      }
+    } else if constexpr (BPT > 0 && MODE == MODE_POLY) {
 #pragma unroll
       for (int b = 0; b < BPT; ++b)
         bin_poly<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
