@@ -35,6 +35,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 N_BINS, NN, CHAINS, WARMUP_IT, SAMPLES = 2048, 15, 1024, 500, 1000
+# BASELINE.json configs that run on the sampler (--config K = configs[K-1]).  The
+# headline line is config 3; 2 and 4 are secondary measurements (config 4's
+# 8192 chains are 1024 per GPU over 8 GPUs: weak scaling of the same per-GPU shape).
+CONFIGS = {
+    2: dict(prior="normal", N=512, chains=128),
+    3: dict(prior="horseshoe", N=2048, chains=1024),
+    4: dict(prior="lasso", N=4096, chains=1024),
+    # FitOCT.R batch mode: 256 synthetic files (the 4 modulations of synthData.R:21,35,49,
+    # 63 at N=481), 4 chains each, ctrlParams.yaml's 100 warmup + 100 draws, Nn=15
+    # extremal, normal prior; files sharded round-robin over the ranks (strong scaling)
+    5: dict(prior="normal", N=481, chains=4, files=256, iters=(100, 100)),
+}
 FP64_VALU_PEAK_TF = 78.6          # MI355X FP64 vector peak (vendor spec; 1/2 of FP32 vector)
 HBM_PEAK_GBS = 8000.0
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
@@ -44,13 +56,14 @@ def f_grad(N, Nn):
     return 4 * N * Nn + 20 * N     # SURVEY.md §8d algorithmic flop per gradient
 
 
-def make_problem():
+def make_problem(prior="horseshoe", N=N_BINS):
     from fitoct_amd import ExpGPProblem
     from fitoct_amd.synth import default_prior, synth_decay
     t0, S0 = default_prior()
-    d = synth_decay(N_BINS, "sincExp", 1234)
+    d = synth_decay(N, "sincExp", 1234)
+    # lasso lambda_s = 10 mirrors Tests/testGamma.R:35
     return ExpGPProblem(d["x"], d["y"], d["uy"], dataType=2, Nn=NN, gridType="extremal",
-                        theta0=t0, Sigma0=S0, prior_type="horseshoe", nu=1.0)
+                        theta0=t0, Sigma0=S0, prior_type=prior, nu=1.0, lambda_scale=10.0)
 
 
 def make_config(seed, chains, offset, device, warmup_it, samples):
@@ -101,12 +114,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--chains", type=int, default=CHAINS, help="chains per GPU")
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[K-1]; 3 is the headline")
+    ap.add_argument("--chains", type=int, default=0, help="chains per GPU (0: the config's)")
     ap.add_argument("--iters", type=str, default=f"{WARMUP_IT},{SAMPLES}",
                     help="sampler warmup,samples per chain")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--precision", default="f64", choices=["f64", "mixed"])
     args = ap.parse_args()
+    if args.config == 5 and args.iters == f"{WARMUP_IT},{SAMPLES}":
+        args.iters = "%d,%d" % CONFIGS[5]["iters"]
     W_it, S_it = (int(v) for v in args.iters.split(","))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,12 +150,17 @@ def main():
     torch.cuda.set_device(dev)
     cdev = dev if backend == "nccl" else torch.device("cpu")   # where collectives run
 
+    if args.config == 5:
+        return bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it)
+
     from fitoct_amd import Plan
     from fitoct_amd.api import SamplerConfig  # noqa: F401  (import check)
     from fitoct_amd.stanfit import split_rhat_ess
 
-    prob = make_problem()
-    C = args.chains
+    conf = CONFIGS[args.config]
+    N_bins = conf["N"]
+    prob = make_problem(conf["prior"], N_bins)
+    C = args.chains or conf["chains"]
     offset = rank * C
 
     def plan_for(step):
@@ -214,17 +236,17 @@ def main():
     divergent = float(last[:, W_saved:, 5].mean())
     lf_per_draw = float(np.mean(lf_steps)) / (C * (W_it + S_it))
 
-    workload = (f"fitExpGP+horseshoe N={N_BINS} Nn={NN} {C} chains/GPU "
+    workload = (f"fitExpGP+{conf['prior']} N={N_bins} Nn={NN} {C} chains/GPU "
                 f"W={W_it} S={S_it} treedepth<=10")
     kms = float(np.mean(kernel_ms))
-    flops = f_grad(N_BINS, NN) * float(np.mean(lf_steps))
+    flops = f_grad(N_bins, NN) * float(np.mean(lf_steps))
     achieved = flops / (kms / 1e3) / 1e12
     traffic = load_traffic(workload)
     roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TF,
             "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TF, 4),
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "kernel": "nuts_kernel", "kernel_ms": round(kms, 2),
-            "flop_per_gradient": f_grad(N_BINS, NN),
+            "flop_per_gradient": f_grad(N_bins, NN),
             "gradients_per_launch": int(np.mean(lf_steps))}
     if traffic:
         roof["hbm_gbs"] = round(traffic["bytes_per_launch"] / (kms / 1e3) / 1e9, 2)
@@ -232,12 +254,13 @@ def main():
         roof["traffic_source"] = os.path.relpath(TRAFFIC_FILE, ROOT)
 
     line = {
-        "metric": "posterior draws/sec (all chains), ExpGP N=2048 @ 1024 chains; R-hat",
+        "metric": ("posterior draws/sec (all chains), ExpGP N=2048 @ 1024 chains; R-hat"
+                   if args.config == 3 else f"posterior draws/sec (all chains), config {args.config}"),
         "value": round(value, 2), "unit": "draws/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64" if args.precision == "f64"
         else "f32-sweep/f64-state", "data": "synthetic (restated synthData.R sincExp decay)",
-        "config": {"workload": workload, "prior": "horseshoe", "N": N_BINS, "Nn": NN,
+        "config": {"workload": workload, "prior": conf["prior"], "N": N_bins, "Nn": NN,
                    "chains_per_gpu": C, "global_chains": world * C, "warmup_iters": W_it,
                    "samples": S_it, "adapt_delta": 0.8, "max_treedepth": 10,
                    "parallelism": f"chains sharded over {world} GPU(s)"},
@@ -251,6 +274,108 @@ def main():
         line["cpu_baseline"] = cpu_baseline(prob, float(np.mean(lf_steps)), C * S_it)
     for pl in plans:
         pl.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
+    """Config 5 (FitOCT.R batch mode): this rank's files in ONE batched launch
+    (fitoct_batch_*); one gather of every rank's draws to rank 0 inside the step."""
+    import torch
+    from fitoct_amd import Batch, ExpGPProblem, SamplerConfig
+    from fitoct_amd.stanfit import split_rhat_ess
+    from fitoct_amd.synth import MODULATIONS, default_prior, synth_decay
+
+    conf = CONFIGS[5]
+    t0, S0 = default_prior()
+    files = list(range(rank, conf["files"], world))     # round-robin by file
+    probs = []
+    for f in files:
+        d = synth_decay(conf["N"], MODULATIONS[f % 4], 1234 + f)
+        probs.append(ExpGPProblem(d["x"], d["y"], d["uy"], dataType=2, Nn=NN,
+                                  gridType="extremal", theta0=t0, Sigma0=S0,
+                                  prior_type=conf["prior"]))
+    C = args.chains or conf["chains"]
+
+    def batch_for(step):
+        cfg = SamplerConfig(chains=C, warmup=W_it, samples=S_it, seed=2000 + step,
+                            adapt_delta=0.8, max_treedepth=10, device=local)
+        return Batch(probs, cfg)
+
+    stream = torch.cuda.current_stream(dev)
+    bufs = {}
+
+    def run_step(b):
+        key = b.info["draws_bytes"]
+        if key not in bufs:
+            bufs[key] = torch.empty(key // 8, dtype=torch.float64, device=dev)
+        buf = bufs[key]
+        b.run(d_draws=buf.data_ptr(), stream=stream.cuda_stream)
+        if world > 1:   # ragged file counts per rank: all_gather of sizes, then gather
+            src = buf if backend == "nccl" else buf.cpu()
+            n = torch.tensor([src.numel()], dtype=torch.int64, device=cdev)
+            sizes = [torch.zeros_like(n) for _ in range(world)]
+            dist.all_gather(sizes, n)
+            m = int(max(int(x.item()) for x in sizes))
+            pad = torch.zeros(m, dtype=torch.float64, device=src.device)
+            pad[:src.numel()] = src
+            gl = [torch.empty(m, dtype=torch.float64, device=src.device)
+                  for _ in range(world)] if rank == 0 else None
+            dist.gather(pad, gather_list=gl, dst=0)
+
+    for w in range(args.warmup):
+        with batch_for(-1 - w) as b:
+            run_step(b)
+    torch.cuda.synchronize()
+    batches = [batch_for(s) for s in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_0 = time.perf_counter()
+    for b in batches:
+        run_step(b)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t_0
+    if dist is not None:
+        t = torch.tensor([wall], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    last = batches[-1]
+    outs = [last.download(p) for p in range(len(probs))]
+    kernel_ms = float(np.mean([b.download(0, with_draws=False).kernel_ms for b in batches]))
+    lf = sum(o.total_leapfrogs for o in outs)
+    cols = probs[0].column_names()
+    par = [j for j in range(7, len(cols))]
+    rh_file = [max(split_rhat_ess(o.draws[:, o.warmup_saved:, j])[0] for j in par) for o in outs]
+    ms_per_step = wall * 1e3 / args.steps
+    draws_step = conf["files"] * C * S_it
+    achieved = f_grad(conf["N"], NN) * lf / (kernel_ms / 1e3) / 1e12
+    line = {
+        "metric": "posterior draws/sec (all chains), config 5 (FitOCT.R batch mode)",
+        "value": round(draws_step / (ms_per_step / 1e3), 2), "unit": "draws/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (restated synthData.R, 4 modulations cycled over files)",
+        "config": {"workload": f"FitOCT.R batch: {conf['files']} files x {C} chains, "
+                               f"fitExpGP+{conf['prior']} N={conf['N']} Nn={NN} W={W_it} S={S_it}",
+                   "files": conf["files"], "files_this_rank": len(files), "chains_per_file": C,
+                   "parallelism": f"files round-robin over {world} GPU(s), one launch per GPU"},
+        "rhat_max_median_file": round(float(np.median(rh_file)), 4),
+        "rhat_max_worst_file": round(float(np.max(rh_file)), 4),
+        "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TF,
+                     "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TF, 4),
+                     "traffic": None, "kernel": "nuts_kernel (batched)",
+                     "kernel_ms": round(kernel_ms, 2), "gradients_per_launch_rank0": lf},
+    }
+    for b in batches:
+        b.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

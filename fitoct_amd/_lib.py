@@ -131,6 +131,12 @@ SIGNATURES = [
     ("fitoct_plan_run", C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("fitoct_plan_download", C.c_int32, [C.c_void_p, C.POINTER(Result)]),
     ("fitoct_plan_destroy", None, [C.c_void_p]),
+    ("fitoct_batch_create", C.c_int32,
+     [C.POINTER(Problem), C.c_int32, C.POINTER(Config), C.POINTER(C.c_void_p)]),
+    ("fitoct_batch_get_info", C.c_int32, [C.c_void_p, C.POINTER(PlanInfo)]),
+    ("fitoct_batch_run", C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fitoct_batch_download", C.c_int32, [C.c_void_p, C.c_int32, C.POINTER(Result)]),
+    ("fitoct_batch_destroy", None, [C.c_void_p]),
     ("fitoct_evaluator_create", C.c_int32,
      [C.POINTER(Problem), C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     ("fitoct_evaluator_run", C.c_int32,

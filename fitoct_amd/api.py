@@ -239,6 +239,84 @@ class Plan:
         self.close()
 
 
+class Batch:
+    """Many problems (FitOCT.R's per-file fits, FitOCT.R:70-124) sampled by one
+    launch (``fitoct_batch_*``).  Problem ``p``'s chains are global chains
+    ``cfg.chain_offset + p*cfg.chains + c``, so its draws equal a :class:`Plan`
+    of that problem with ``chain_offset = cfg.chain_offset + p*cfg.chains``."""
+
+    def __init__(self, probs, cfg: SamplerConfig):
+        self.probs, self.cfg = list(probs), cfg
+        if not self.probs:
+            raise ValueError("a batch needs at least one problem")
+        arr = (_lib.Problem * len(self.probs))()
+        for i, p in enumerate(self.probs):
+            arr[i] = p.to_c()
+        self._arr = arr    # the problems' numpy buffers stay referenced by self.probs
+        self._c = cfg.to_c()
+        h = C.c_void_p()
+        check(lib().fitoct_batch_create(arr, len(self.probs), C.byref(self._c), C.byref(h)))
+        self._h = h
+        info = _lib.PlanInfo()
+        check(lib().fitoct_batch_get_info(self._h, C.byref(info)))
+        self.info = {f: getattr(info, f) for f, _ in _lib.PlanInfo._fields_}
+
+    def __len__(self):
+        return len(self.probs)
+
+    def run(self, d_draws: int = 0, stream: int = 0):
+        """One launch for every problem; draws to ``d_draws`` (device pointer,
+        >= info['draws_bytes'], layout [problem][chain][iter][col]) or internal."""
+        check(lib().fitoct_batch_run(self._h, C.c_void_p(d_draws or None),
+                                     C.c_void_p(stream or None)))
+
+    def download(self, problem: int, with_draws: bool = True) -> SampleOutput:
+        i, C_ = self.info, self.cfg.chains
+        D = i["dim"]
+        draws = np.empty((C_, i["iters_saved"], i["n_cols"])) if with_draws else None
+        eps, minv, lq = np.empty(C_), np.empty((C_, D)), np.empty((C_, D))
+        st = np.zeros(C_, dtype=np.int32)
+        r = _lib.Result()
+        r.draws = dptr(draws)
+        r.draws_capacity = draws.size if with_draws else 0
+        r.stepsize, r.inv_metric, r.last_q = dptr(eps), dptr(minv), dptr(lq)
+        r.chain_status = st.ctypes.data_as(C.POINTER(C.c_int32))
+        check(lib().fitoct_batch_download(self._h, int(problem), C.byref(r)))
+        return SampleOutput(draws, self.probs[problem].column_names(),
+                            self.cfg.warmup if self.cfg.save_warmup else 0, eps, minv, lq,
+                            int(r.total_leapfrogs), float(r.kernel_ms), 0.0,
+                            self.cfg.chain_offset + problem * C_)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().fitoct_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def sample_batch(probs, cfg: SamplerConfig):
+    """One launch over every problem; returns one SampleOutput per problem."""
+    t0 = time.perf_counter()
+    with Batch(probs, cfg) as b:
+        b.run()
+        outs = [b.download(p) for p in range(len(b))]
+    wall = (time.perf_counter() - t0) * 1e3
+    for o in outs:
+        o.wall_ms = wall
+    return outs
+
+
 def sample(prob: ExpGPProblem, cfg: SamplerConfig) -> SampleOutput:
     """One-shot sampler run (plan + run + download)."""
     t0 = time.perf_counter()

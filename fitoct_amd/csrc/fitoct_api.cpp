@@ -18,21 +18,22 @@
 
 namespace fitoct {
 hipError_t launch_family_0(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
-                           const KParams* dP, int tiles, hipStream_t st);
+                           const KParams* dP, int tiles, hipStream_t st, const int* tile_map);
 hipError_t launch_family_1(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
-                           const KParams* dP, int tiles, hipStream_t st);
+                           const KParams* dP, int tiles, hipStream_t st, const int* tile_map);
 hipError_t launch_family_2(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
-                           const KParams* dP, int tiles, hipStream_t st);
+                           const KParams* dP, int tiles, hipStream_t st, const int* tile_map);
 hipError_t launch_family_3(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
-                           const KParams* dP, int tiles, hipStream_t st);
+                           const KParams* dP, int tiles, hipStream_t st, const int* tile_map);
 // the sampler is compiled per prior family (nuts_device.hip, -DFITOCT_FAMILY)
 inline hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
-                         const KParams* dP, int tiles, hipStream_t st) {
+                         const KParams* dP, int tiles, hipStream_t st,
+                         const int* tile_map = nullptr) {
   switch (P.family) {
-    case 0: return launch_family_0(logp, mixed, bpt, nnp, P, dP, tiles, st);
-    case 1: return launch_family_1(logp, mixed, bpt, nnp, P, dP, tiles, st);
-    case 2: return launch_family_2(logp, mixed, bpt, nnp, P, dP, tiles, st);
-    case 3: return launch_family_3(logp, mixed, bpt, nnp, P, dP, tiles, st);
+    case 0: return launch_family_0(logp, mixed, bpt, nnp, P, dP, tiles, st, tile_map);
+    case 1: return launch_family_1(logp, mixed, bpt, nnp, P, dP, tiles, st, tile_map);
+    case 2: return launch_family_2(logp, mixed, bpt, nnp, P, dP, tiles, st, tile_map);
+    case 3: return launch_family_3(logp, mixed, bpt, nnp, P, dP, tiles, st, tile_map);
     default: return hipErrorInvalidValue;
   }
 }
@@ -275,7 +276,7 @@ void stage(const fitoct_problem* p, const std::vector<double>& B, const std::vec
 
 // common planning for the sampler and the logp kernel
 int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precision, int device,
-                int max_depth) {
+                int max_depth, int g_chains = 0, int force_bpt = -1) {
   int rc = check_problem(p);
   if (rc) return rc;
   int ndev = 0;
@@ -320,6 +321,11 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   // f64 rows (NNP doubles per bin) are always streamed
   int n_pad;
   choose_bins(p->N, mode == MODE_POLY ? 8 : pl->mixed ? 4 : 0, pl->bpt, n_pad);
+  if (force_bpt >= 0 && force_bpt != pl->bpt) {   // batch: the batch's common bin layout
+    if (force_bpt != 0 && force_bpt < pl->bpt) return fail(FITOCT_E_ARG, "bin layout too small");
+    pl->bpt = force_bpt;
+    n_pad = force_bpt ? force_bpt * GT : (p->N + GT - 1) / GT * GT;
+  }
   std::vector<char> staged;
   if (pl->mixed) stage<float>(p, B, ta, mode, n_pad, pl->nnp, staged);
   else stage<double>(p, B, ta, mode, n_pad, pl->nnp, staged);
@@ -364,7 +370,9 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
 
   // chains per tile: fill every CU with one tile first, then stack chains
   const int ncu = std::max(1, prop.multiProcessorCount);
-  int G = std::max(1, std::min(GMAX, (chains + ncu - 1) / ncu));
+  // (a batch plans every problem's tiles from the batch's total chain count)
+  const int gc = g_chains > 0 ? g_chains : chains;
+  int G = std::max(1, std::min(GMAX, (gc + ncu - 1) / ncu));
   while (G > 1 && lds_bytes(pl->ppl, G, max_depth) > 160 * 1024 - 256) --G;
   if (lds_bytes(pl->ppl, G, max_depth) > 160 * 1024 - 256)
     return fail(FITOCT_E_ARG, "max_treedepth too large for the LDS budget");
@@ -374,6 +382,9 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   pl->lds = lds_bytes(pl->ppl, G, max_depth);
   return FITOCT_OK;
 }
+
+int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chains,
+                int force_bpt, fitoct_plan** out);
 
 void free_plan(fitoct_plan* pl) {
   if (!pl) return;
@@ -573,6 +584,14 @@ int32_t fitoct_logp_grad(const fitoct_problem* prob, int32_t n_points, const dou
 
 int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
                            fitoct_plan** out) {
+  return plan_create(prob, cfg, 0, -1, out);
+}
+
+}  // extern "C"
+
+namespace {
+int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chains,
+                int force_bpt, fitoct_plan** out) {
   if (!out) return fail(FITOCT_E_ARG, "out is NULL");
   *out = nullptr;
   if (!cfg) return fail(FITOCT_E_ARG, "config is NULL");
@@ -584,7 +603,8 @@ int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
     return fail(FITOCT_E_ARG, "adapt_delta must be in (0, 1)");
   if (!(cfg->stepsize > 0.0)) return fail(FITOCT_E_ARG, "stepsize must be > 0");
   fitoct_plan* pl = new fitoct_plan();
-  int rc = plan_common(pl, prob, cfg->chains, cfg->precision, cfg->device, cfg->max_treedepth);
+  int rc = plan_common(pl, prob, cfg->chains, cfg->precision, cfg->device, cfg->max_treedepth,
+                       g_chains, force_bpt);
   if (rc) {
     free_plan(pl);
     return rc;
@@ -637,6 +657,9 @@ int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
   *out = pl;
   return FITOCT_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
   if (!pl || !info) return fail(FITOCT_E_ARG, "NULL argument");
@@ -802,5 +825,171 @@ int32_t fitoct_rank_rhat(const double* x, int32_t chains, int32_t n, double* rha
   if (!x || !rhat) return fail(FITOCT_E_ARG, "NULL argument");
   return rank_rhat(x, chains, n, rhat);
 }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Batch mode: many problems (FitOCT.R's per-file fitExpGP calls, FitOCT.R:70-124)
+// sampled by ONE persistent launch.  Each problem keeps its own staged data,
+// basis factors, pool and outputs (a fitoct_plan each); the kernel receives the
+// array of their parameter blocks and a tile map {problem, first chain}, so a
+// tile only ever holds one problem's chains.  Chain c of problem p is keyed as
+// global chain cfg.chain_offset + p*chains + c: its draws are those of a single
+// plan of that problem with chain_offset = cfg.chain_offset + p*chains.
+// ---------------------------------------------------------------------------
+struct fitoct_batch {
+  std::vector<fitoct_plan*> plans;
+  fitoct_config cfg{};
+  int tiles = 0;
+  size_t per_bytes = 0;       // draws bytes of one problem
+  KParams* d_kp = nullptr;    // [n_problems]
+  int* d_map = nullptr;       // [tiles][2]
+  double* d_draws = nullptr;  // internal [n_problems][chains][iters][cols] (lazy)
+  double kernel_ms = 0.0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool ran = false;
+};
+
+namespace {
+void free_batch(fitoct_batch* b) {
+  if (!b) return;
+  for (fitoct_plan* pl : b->plans) free_plan(pl);
+  (void)hipFree(b->d_kp);
+  (void)hipFree(b->d_map);
+  (void)hipFree(b->d_draws);
+  if (b->ev0) (void)hipEventDestroy(b->ev0);
+  if (b->ev1) (void)hipEventDestroy(b->ev1);
+  delete b;
+}
+}  // namespace
+
+extern "C" {
+
+int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
+                            const fitoct_config* cfg, fitoct_batch** out) {
+  if (!out) return fail(FITOCT_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (!probs || n_problems < 1) return fail(FITOCT_E_ARG, "need n_problems >= 1 problems");
+  if (!cfg) return fail(FITOCT_E_ARG, "config is NULL");
+  if (cfg->chains < 1) return fail(FITOCT_E_ARG, "chains must be >= 1");
+  if ((int64_t)n_problems * cfg->chains > (int64_t)1 << 30)
+    return fail(FITOCT_E_ARG, "too many chains in one batch");
+  fitoct_batch* b = new fitoct_batch();
+  b->cfg = *cfg;
+  const int C = cfg->chains;
+  auto build = [&]() -> int {
+    for (int p = 0; p < n_problems; ++p) {
+      if (probs[p].prior_type != probs[0].prior_type || probs[p].Nn != probs[0].Nn)
+        return fail(FITOCT_E_ARG, "batch problems must share prior_type and Nn (problem " +
+                                      std::to_string(p) + ")");
+      fitoct_config c = *cfg;
+      c.chain_offset = cfg->chain_offset + p * C;
+      fitoct_plan* pl = nullptr;
+      const int rc = plan_create(&probs[p], &c, n_problems * C, -1, &pl);
+      if (rc) return fail(rc, "problem " + std::to_string(p) + ": " + fitoct_last_error());
+      b->plans.push_back(pl);
+    }
+    // one kernel instantiation and one LDS carve must serve every problem
+    int bpt = 0;
+    for (fitoct_plan* pl : b->plans) bpt = std::max(bpt, pl->bpt == 0 ? 1 << 20 : pl->bpt);
+    const fitoct_plan* p0 = b->plans[0];
+    for (fitoct_plan* pl : b->plans) {
+      if (pl->kp.mode != p0->kp.mode || pl->nnp != p0->nnp || pl->ppl != p0->ppl ||
+          pl->mixed != p0->mixed || pl->kp.G != p0->kp.G)
+        return fail(FITOCT_E_ARG, "batch problems plan to different kernels (basis mode)");
+    }
+    // bins: every tile runs the batch's widest bin layout.  A problem planned with
+    // fewer bins per lane is restaged at the common n_pad (zero-weight padding).
+    if (bpt == 1 << 20) bpt = 0;
+    for (size_t p = 0; p < b->plans.size(); ++p) {
+      fitoct_plan* pl = b->plans[p];
+      if (pl->bpt == bpt) continue;
+      fitoct_config c = *cfg;
+      c.chain_offset = cfg->chain_offset + (int)p * C;
+      free_plan(pl);
+      b->plans[p] = nullptr;
+      const int rc = plan_create(&probs[p], &c, n_problems * C, bpt, &b->plans[p]);
+      if (rc) return rc;
+    }
+    b->per_bytes = b->plans[0]->draws_bytes;
+    std::vector<int> map;
+    const int G = b->plans[0]->kp.G;
+    for (int p = 0; p < n_problems; ++p)
+      for (int c0 = 0; c0 < C; c0 += G) {
+        map.push_back(p);
+        map.push_back(c0);
+      }
+    b->tiles = (int)map.size() / 2;
+    HIP_TRY(hipSetDevice(cfg->device));
+    HIP_TRY(hipMalloc(&b->d_map, sizeof(int) * map.size()));
+    HIP_TRY(hipMemcpy(b->d_map, map.data(), sizeof(int) * map.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&b->d_kp, sizeof(KParams) * n_problems));
+    HIP_TRY(hipEventCreate(&b->ev0));
+    HIP_TRY(hipEventCreate(&b->ev1));
+    return FITOCT_OK;
+  };
+  const int rc = build();
+  if (rc) {
+    free_batch(b);
+    return rc;
+  }
+  *out = b;
+  return FITOCT_OK;
+}
+
+int32_t fitoct_batch_get_info(const fitoct_batch* b, fitoct_plan_info* info) {
+  if (!b || !info) return fail(FITOCT_E_ARG, "NULL argument");
+  const int rc = fitoct_plan_get_info(b->plans[0], info);
+  if (rc) return rc;
+  info->chains = b->cfg.chains * (int)b->plans.size();
+  info->tiles = b->tiles;
+  info->draws_bytes = (int64_t)(b->per_bytes * b->plans.size());
+  return FITOCT_OK;
+}
+
+int32_t fitoct_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
+  if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
+  HIP_TRY(hipSetDevice(b->cfg.device));
+  const size_t P = b->plans.size();
+  double* dst = (double*)d_draws;
+  if (!dst) {
+    if (!b->d_draws) HIP_TRY(hipMalloc(&b->d_draws, b->per_bytes * P));
+    dst = b->d_draws;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<KParams> kp(P);
+  for (size_t p = 0; p < P; ++p) {
+    fitoct_plan* pl = b->plans[p];
+    kp[p] = pl->kp;
+    kp[p].draws = (double*)((char*)dst + b->per_bytes * p);
+    pl->last_draws = kp[p].draws;
+    HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * pl->kp.chains, st));
+  }
+  HIP_TRY(hipMemcpyAsync(b->d_kp, kp.data(), sizeof(KParams) * P, hipMemcpyHostToDevice, st));
+  const fitoct_plan* p0 = b->plans[0];
+  HIP_TRY(hipEventRecord(b->ev0, st));
+  HIP_TRY(launch(false, p0->mixed, p0->bpt, p0->nnp, kp[0], b->d_kp, b->tiles, st, b->d_map));
+  HIP_TRY(hipEventRecord(b->ev1, st));
+  HIP_TRY(hipEventSynchronize(b->ev1));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->kernel_ms = ms;
+  for (fitoct_plan* pl : b->plans) {
+    pl->kernel_ms = ms;
+    pl->ran = true;
+  }
+  b->ran = true;
+  return FITOCT_OK;
+}
+
+int32_t fitoct_batch_download(fitoct_batch* b, int32_t problem, fitoct_result* res) {
+  if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
+  if (problem < 0 || problem >= (int32_t)b->plans.size())
+    return fail(FITOCT_E_ARG, "problem index out of range");
+  if (!b->ran) return fail(FITOCT_E_ARG, "batch has not run");
+  return fitoct_plan_download(b->plans[problem], res);
+}
+
+void fitoct_batch_destroy(fitoct_batch* b) { free_batch(b); }
 
 }  // extern "C"

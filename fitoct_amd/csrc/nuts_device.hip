@@ -1539,14 +1539,27 @@ constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded,
 // until grad_cnt[c] reaches NGW * epoch and runs the sampler until it yields
 // the next position.  Chains cycle independently (no barrier after start-up),
 // so the sampler latency of one chain hides behind the sweeps of the others.
+//
+// Batch mode (fitoct_batch_*, FitOCT.R's loop over files): Pg is an array of
+// parameter blocks, one per problem, and tile_map[2*tile] = {problem, first
+// chain} places each tile; a tile never mixes problems, so every tile still
+// keeps one problem's bins in registers.  tile_map == nullptr: one problem.
 template <class R, int BPT, int NNP, int PPL, int MODE, int FAM>
-__global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict__ Pg) {
-  KPc& P = *(KPc*)Pg;   // device-resident parameter block: uniform s_load reads
+__global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict__ Pg,
+                                                      const int* __restrict__ tile_map) {
+  int pidx = 0, c0;
+  if (tile_map) {
+    const AS_CST int* tm = (const AS_CST int*)tile_map;
+    pidx = __builtin_amdgcn_readfirstlane(tm[2 * blockIdx.x]);
+    c0 = __builtin_amdgcn_readfirstlane(tm[2 * blockIdx.x + 1]);
+  } else {
+    c0 = blockIdx.x * ((KPc*)Pg)->G;
+  }
+  KPc& P = *((KPc*)Pg + pidx);   // device-resident parameter block: uniform s_load reads
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const Lds<PPL> L{(AS_LDS char*)smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int c0 = blockIdx.x * P.G;
   const int nct = min(P.G, P.chains - c0);
   __shared__ unsigned long long ring[RINGN];
   __shared__ int q_reserve, n_active, grad_cnt[GMAX];
@@ -1777,7 +1790,7 @@ int lds_bytes(int ppl, int G, int max_depth) {
 
 template <class R, int BPT, int NNP, int PPL, int MODE>
 static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int tiles,
-                           hipStream_t st) {
+                           hipStream_t st, const int* tile_map) {
   constexpr int F = FITOCT_FAMILY;
   const int lds = Lds<PPL>::bytes(P.G, P.max_depth);
   if (logp) {
@@ -1787,21 +1800,21 @@ static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int t
   } else {
     auto k = nuts_kernel<R, BPT, NNP, PPL, MODE, F>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP);
+    hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP, tile_map);
   }
   return hipGetLastError();
 }
 
 template <class R, int NNP, int PPL, int MODE>
 static hipError_t launch_m(bool logp, int bpt, const KParams& P, const KParams* dP, int tiles,
-                           hipStream_t st) {
+                           hipStream_t st, const int* tm) {
   switch (bpt) {
-    case 0: return launch_t<R, 0, NNP, PPL, MODE>(logp, P, dP, tiles, st);
-    case 1: return launch_t<R, 1, NNP, PPL, MODE>(logp, P, dP, tiles, st);
-    case 2: return launch_t<R, 2, NNP, PPL, MODE>(logp, P, dP, tiles, st);
-    case 4: return launch_t<R, 4, NNP, PPL, MODE>(logp, P, dP, tiles, st);
+    case 0: return launch_t<R, 0, NNP, PPL, MODE>(logp, P, dP, tiles, st, tm);
+    case 1: return launch_t<R, 1, NNP, PPL, MODE>(logp, P, dP, tiles, st, tm);
+    case 2: return launch_t<R, 2, NNP, PPL, MODE>(logp, P, dP, tiles, st, tm);
+    case 4: return launch_t<R, 4, NNP, PPL, MODE>(logp, P, dP, tiles, st, tm);
     case 8:
-      if constexpr (MODE == MODE_POLY) return launch_t<R, 8, NNP, PPL, MODE>(logp, P, dP, tiles, st);
+      if constexpr (MODE == MODE_POLY) return launch_t<R, 8, NNP, PPL, MODE>(logp, P, dP, tiles, st, tm);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -1809,23 +1822,25 @@ static hipError_t launch_m(bool logp, int bpt, const KParams& P, const KParams* 
 
 template <int NNP, int PPL>
 static hipError_t launch_n(bool logp, bool mixed, int bpt, const KParams& P, const KParams* dP,
-                           int tiles, hipStream_t st) {
+                           int tiles, hipStream_t st, const int* tm) {
   if (!mixed) {
-    if (P.mode == MODE_POLY) return launch_m<double, NNP, PPL, MODE_POLY>(logp, bpt, P, dP, tiles, st);
-    return launch_t<double, 0, NNP, PPL, MODE_ROWS>(logp, P, dP, tiles, st);
+    if (P.mode == MODE_POLY)
+      return launch_m<double, NNP, PPL, MODE_POLY>(logp, bpt, P, dP, tiles, st, tm);
+    return launch_t<double, 0, NNP, PPL, MODE_ROWS>(logp, P, dP, tiles, st, tm);
   }
-  return launch_m<float, NNP, PPL, MODE_ROWS>(logp, bpt, P, dP, tiles, st);
+  return launch_m<float, NNP, PPL, MODE_ROWS>(logp, bpt, P, dP, tiles, st, tm);
 }
 
 // P: host copy (shapes); dP: the same block already copied to device memory
 hipError_t FITOCT_CAT(launch_family_, FITOCT_FAMILY)(bool logp, bool mixed, int bpt, int nnp,
                                                      const KParams& P, const KParams* dP,
-                                                     int tiles, hipStream_t st) {
+                                                     int tiles, hipStream_t st,
+                                                     const int* tile_map) {
 #ifdef FITOCT_ONE_VARIANT
-  return launch_t<double, 8, 16, 1, MODE_POLY>(logp, P, dP, tiles, st);
+  return launch_t<double, 8, 16, 1, MODE_POLY>(logp, P, dP, tiles, st, tile_map);
 #else
-  if (nnp == 16) return launch_n<16, 1>(logp, mixed, bpt, P, dP, tiles, st);
-  return launch_n<24, 2>(logp, mixed, bpt, P, dP, tiles, st);
+  if (nnp == 16) return launch_n<16, 1>(logp, mixed, bpt, P, dP, tiles, st, tile_map);
+  return launch_n<24, 2>(logp, mixed, bpt, P, dP, tiles, st, tile_map);
 #endif
 }
 

@@ -179,6 +179,24 @@ int32_t fitoct_plan_run(fitoct_plan* plan, void* d_draws, void* stream);
 int32_t fitoct_plan_download(fitoct_plan* plan, fitoct_result* res);
 void fitoct_plan_destroy(fitoct_plan* plan);
 
+/* ---- batch mode ---------------------------------------------------------- *
+ * Replaces FitOCT.R's per-file loop (FitOCT.R:70-124: one FitOCTLib::fitExpGP ->
+ * rstan::sampling call per Courbe.csv) with ONE persistent launch sampling every
+ * file's chains: `n_problems` problems sharing prior_type and Nn, each with
+ * cfg->chains chains (a tile never mixes files).  Chain c of problem p is keyed
+ * as global chain cfg->chain_offset + p*cfg->chains + c, so problem p's draws
+ * equal a single plan of it with chain_offset = cfg->chain_offset + p*chains.
+ * Draws land in [n_problems][chains][iters_saved][n_cols] (caller device buffer
+ * of info.draws_bytes, or internal).  Caller buffers are not retained. */
+typedef struct fitoct_batch fitoct_batch;
+int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
+                            const fitoct_config* cfg, fitoct_batch** out);
+int32_t fitoct_batch_get_info(const fitoct_batch* batch, fitoct_plan_info* info);
+int32_t fitoct_batch_run(fitoct_batch* batch, void* d_draws, void* stream);
+/* outputs of problem `problem` (draws of that problem only), as fitoct_plan_download */
+int32_t fitoct_batch_download(fitoct_batch* batch, int32_t problem, fitoct_result* res);
+void fitoct_batch_destroy(fitoct_batch* batch);
+
 /* ---- batched density evaluator ------------------------------------------- *
  * The model of a problem staged once in HBM, evaluated at up to `capacity`
  * points per call by the same kernel as fitoct_logp_grad (which is a one-shot
