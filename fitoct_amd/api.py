@@ -178,6 +178,7 @@ class SampleOutput:
     kernel_ms: float
     wall_ms: float
     chain_offset: int = 0
+    migrations: int = 0        # chains handed between tiles (work balance)
 
 
 class Plan:
@@ -219,7 +220,7 @@ class Plan:
         return SampleOutput(draws, self.prob.column_names(),
                             self.cfg.warmup if self.cfg.save_warmup else 0, eps, minv, lq,
                             int(r.total_leapfrogs), float(r.kernel_ms), 0.0,
-                            self.cfg.chain_offset)
+                            self.cfg.chain_offset, int(r.migrations))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -38,6 +38,7 @@ inline hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams&
   }
 }
 int lds_bytes(int ppl, int G, int max_depth);
+int mig_img_words(int ppl);
 }  // namespace fitoct
 
 using namespace fitoct;
@@ -53,8 +54,11 @@ struct fitoct_plan {
   fitoct_problem prob{};
   fitoct_config cfg{};
   KParams kp{};
-  int tiles = 0, bpt = 0, nnp = 16, ppl = 1, lds = 0;
+  int tiles = 0, bpt = 0, nnp = 16, ppl = 1, lds = 0, ncu = 0;
   bool mixed = false;
+  int* d_mig = nullptr;       // chain-migration control block (see MigCtrl)
+  double* d_mig_img = nullptr;
+  size_t mig_bytes = 0;
   size_t draws_bytes = 0;
   void* d_data = nullptr;     // cx | y | isu | B  (type R)
   double* d_draws = nullptr;  // internal draws buffer (lazily allocated)
@@ -370,6 +374,7 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
 
   // chains per tile: fill every CU with one tile first, then stack chains
   const int ncu = std::max(1, prop.multiProcessorCount);
+  pl->ncu = ncu;
   // (a batch plans every problem's tiles from the batch's total chain count)
   const int gc = g_chains > 0 ? g_chains : chains;
   int G = std::max(1, std::min(GMAX, (gc + ncu - 1) / ncu));
@@ -395,6 +400,8 @@ void free_plan(fitoct_plan* pl) {
   (void)hipFree(pl->d_status);
   (void)hipFree(pl->d_leap);
   (void)hipFree(pl->d_kp);
+  (void)hipFree(pl->d_mig);
+  (void)hipFree(pl->d_mig_img);
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
   if (pl->ev1) (void)hipEventDestroy(pl->ev1);
   delete pl;
@@ -654,6 +661,28 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   k.fin_q = pl->d_fin + C + (size_t)C * D;
   k.chain_status = pl->d_status;
   k.leapfrogs = pl->d_leap;
+  // Chain migration (work balance): only when every tile of the launch is
+  // co-resident (one tile per CU), so an idle tile waiting for a migrant never
+  // keeps a pending tile off the chip; off in batch mode (a tile holds one
+  // problem's bins) and with FITOCT_NO_MIGRATE.
+  if (g_chains == 0 && k.G >= 2 && pl->tiles <= pl->ncu && getenv("FITOCT_NO_MIGRATE") == nullptr) {
+    const int T = pl->tiles, words = mig_img_words(pl->ppl);
+    pl->mig_bytes = sizeof(int) * (MIG_HDR + 2 * (size_t)T + (size_t)T * GMAX);
+    auto mig_setup = [&]() -> int {
+      HIP_TRY(hipMalloc(&pl->d_mig, pl->mig_bytes));
+      HIP_TRY(hipMalloc(&pl->d_mig_img, sizeof(double) * (size_t)T * GMAX * words));
+      return FITOCT_OK;
+    };
+    rc = mig_setup();
+    if (rc) {
+      free_plan(pl);
+      return rc;
+    }
+    k.mig = pl->d_mig;
+    k.mig_img = pl->d_mig_img;
+    k.mig_tiles = T;
+    k.mig_img_words = words;
+  }
   *out = pl;
   return FITOCT_OK;
 }
@@ -689,6 +718,7 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
   KParams k = pl->kp;
   k.draws = dst;
   HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * k.chains, st));
+  if (pl->d_mig) HIP_TRY(hipMemsetAsync(pl->d_mig, 0, pl->mig_bytes, st));
   long long* d_stamps = nullptr;
   const bool want_stamps = getenv("FITOCT_STAMPS") != nullptr;   // diagnostic only
   if (want_stamps) {
@@ -773,6 +803,9 @@ int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
   res->iters_saved = k.iters_saved;
   res->dim = D;
   res->kernel_ms = pl->kernel_ms;
+  res->migrations = 0;
+  if (pl->d_mig) HIP_TRY(hipMemcpy(&res->migrations, pl->d_mig + MIG_MOVES, sizeof(int),
+                                   hipMemcpyDeviceToHost));
   if (res->draws) {
     const int64_t need = (int64_t)C * k.iters_saved * k.ncols;
     if (res->draws_capacity < need) return fail(FITOCT_E_ARG, "draws buffer too small");

@@ -30,7 +30,17 @@ enum BasisMode : int {
   MODE_ROWS = 1,    // explicit basis rows B[i, 0..NNP) (user basis, fp32 path)
 };
 
-enum ChainState : int { ST_INIT = 0, ST_STEPSIZE = 1, ST_TREE = 2, ST_DONE = 3 };
+enum ChainState : int { ST_INIT = 0, ST_STEPSIZE = 1, ST_TREE = 2, ST_DONE = 3, ST_MOVED = 4 };
+
+// Chain migration between tiles (work balance at the end of a run).  Layout of
+// KParams::mig (int32, zeroed before every launch):
+enum MigCtrl : int {
+  MIG_WAITING = 0,   // NUTS slots posted as free (receivers)
+  MIG_DONE = 1,      // chains finished (ST_DONE) over the whole launch
+  MIG_STARTED = 2,   // tiles that have begun: receivers wait only once all have
+  MIG_MOVES = 3,     // chains handed over (reported in fitoct_result::migrations)
+  MIG_HDR = 4,       // then: load[tiles] | free_mask[tiles] | mailbox[tiles * GMAX]
+};
 
 struct KParams {
   // ---- data (device pointers, padded to n_pad bins) ----
@@ -70,6 +80,10 @@ struct KParams {
   int* chain_status;        // [chains]
   long long* leapfrogs;     // [chains]
   long long* stamps;        // optional [tiles][4]: half-steps, gradient busy, NUTS busy, total cycles
+  // ---- chain migration (nullptr / 0: off) ----
+  int* mig;                 // MigCtrl header | load | free_mask | mailbox (see MigCtrl)
+  double* mig_img;          // [tiles * GMAX][mig_img_words] chain images in flight
+  int mig_tiles, mig_img_words;
   // ---- logp mode ----
   const double* q_in;       // [points][D]
   double* lp_out;           // [points]

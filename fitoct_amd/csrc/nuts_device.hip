@@ -115,6 +115,45 @@ __device__ __forceinline__ void wave_fence() {
 }
 
 // ---------------------------------------------------------------------------
+// chain migration between tiles: agent-scope atomics on global memory (the
+// tiles of a launch sit on different XCDs, each with its own L2; release /
+// acquire at agent scope write back / invalidate L2 as the gfx950 memory model
+// requires).  Rare operations (at most one per transition), so generic pointers.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int g_load(AS_GLB int* p) {
+  return __hip_atomic_load((int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int g_load_acq(AS_GLB int* p) {
+  return __hip_atomic_load((int*)p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_store_rel(AS_GLB int* p, int v) {
+  __hip_atomic_store((int*)p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int g_add(AS_GLB int* p, int v) {
+  return __hip_atomic_fetch_add((int*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int g_or(AS_GLB int* p, int v) {
+  return __hip_atomic_fetch_or((int*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int g_and(AS_GLB int* p, int v) {
+  return __hip_atomic_fetch_and((int*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool g_cas(AS_GLB int* p, int expect, int v) {
+  return __hip_atomic_compare_exchange_strong((int*)p, &expect, v, __ATOMIC_RELAXED,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+struct MigView {   // KParams::mig carved per MigCtrl
+  AS_GLB int* hdr;
+  AS_GLB int* load;
+  AS_GLB int* fmask;
+  AS_GLB int* mbox;
+  __device__ MigView(int* base, int tiles)
+      : hdr((AS_GLB int*)base), load((AS_GLB int*)base + MIG_HDR), fmask(load + tiles),
+        mbox(fmask + tiles) {}
+};
+constexpr unsigned long long MIG_WAIT_TICKS = 120ULL * 100000000ULL;   // 120 s at 100 MHz
+
+// ---------------------------------------------------------------------------
 // cross-lane moves of doubles without LDS (DPP row ops, gfx950 permlane swaps)
 // ---------------------------------------------------------------------------
 constexpr int DPP_XOR1 = 0xB1;         // quad_perm(1,0,3,2)
@@ -1438,7 +1477,62 @@ struct Chain {
     const int t = uni(Sp->t);
     if (t == Pr().warmup && Pr().adapt && Pr().warmup > 0) Sp->eps = exp(Sp->x_bar);  // complete_adaptation
     if (t >= Pr().warmup + Pr().samples) return A_FINISH;
+    // a transition boundary: the chain's whole state is its LDS image (current
+    // sample, metric, adaptation); hand it to an idle tile if this one is crowded
+    if (Pr().mig != nullptr && t + 2 < Pr().warmup + Pr().samples && try_donate()) {
+      Sp->state = ST_MOVED;
+      return A_YIELD;
+    }
     return A_START_TRANSITION;
+  }
+
+  // Work balance (the kernel ends with its slowest tile): a chain in a tile
+  // hosting L chains moves to a posted free slot of a tile hosting <= L-2, if
+  // any.  Its draws do not change: a chain's arithmetic is the same in every
+  // tile of the launch (same bin-to-lane layout) and its random numbers are
+  // addressed by (global chain id, iteration).
+  __device__ bool try_donate() {
+    KPc& P = Pr();
+    const MigView M(P.mig, P.mig_tiles);
+    if (uni(g_load(&M.hdr[MIG_WAITING])) <= 0) return false;
+    const int me = blockIdx.x, T = P.mig_tiles;
+    const int my = uni(g_load(&M.load[me]));
+    if (my < 2) return false;
+    int best = 0x7FFFFFFF;
+    for (int i = lane; i < T; i += WAVE)
+      if (g_load(&M.fmask[i]) != 0) best = min(best, (g_load(&M.load[i]) << 16) | i);
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) best = min(best, __shfl_xor(best, o));
+    best = uni(best);
+    if (best == 0x7FFFFFFF || (best >> 16) > my - 2) return false;
+    const int tt = best & 0xFFFF;
+    int slot = -1;
+    if (lane == 0) {
+      const int f = g_load(&M.fmask[tt]);
+      if (f != 0) {
+        const int b = __builtin_ctz(f);
+        if (g_cas(&M.fmask[tt], f, f & ~(1 << b))) slot = b;
+      }
+    }
+    slot = __shfl(slot, 0);
+    slot = uni(slot);
+    if (slot < 0) return false;
+    if (lane == 0) {
+      g_add(&M.load[tt], 1);
+      g_add(&M.load[me], -1);
+      g_add(&M.hdr[MIG_WAITING], -1);
+      g_add(&M.hdr[MIG_MOVES], 1);
+    }
+    image_out(P.mig_img + (size_t)(tt * GMAX + slot) * P.mig_img_words);
+    __threadfence();
+    if (lane == 0) g_store_rel(&M.mbox[tt * GMAX + slot], lc + 1);
+    return true;
+  }
+  // the chain's LDS state at a transition boundary (scalars, vectors, sums, aux;
+  // the tree levels are dead between transitions) <-> a global image
+  __device__ void image_out(double* dst) const {
+    const AS_LDS double* src = (const AS_LDS double*)Sp;
+    for (int i = lane; i < Pr().mig_img_words; i += WAVE) ((AS_GLB double*)dst)[i] = src[i];
   }
 
   __device__ int act_finish() {
@@ -1532,6 +1626,49 @@ __device__ __forceinline__ unsigned long long lds_load64(const unsigned long lon
 constexpr int RINGN = 16;                 // hand-off ring: >= 2 * GMAX entries
 constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded, never hang a box
 
+// Migration receiver: post NUTS slot c of this tile as free and wait until a
+// crowded tile hands a chain over (returns its chain index, image loaded into
+// the slot's LDS) or every chain of the launch has finished (returns -1).
+// Receivers wait only once every tile of the launch has started: then no tile
+// is waiting for a CU, so waiting cannot starve one.  An idle wait longer than
+// MIG_WAIT_TICKS withdraws the post (if no donor claimed it meanwhile).
+template <int PPL>
+__device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane) {
+  const MigView M(P.mig, P.mig_tiles);
+  const int me = blockIdx.x;
+  if (__builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_STARTED])) < P.mig_tiles) return -1;
+  if (lane == 0) {
+    g_or(&M.fmask[me], 1 << c);
+    g_add(&M.hdr[MIG_WAITING], 1);
+  }
+  AS_GLB int* box = &M.mbox[me * GMAX + c];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  int m = 0;
+  for (;;) {
+    m = __builtin_amdgcn_readfirstlane(g_load_acq(box));
+    if (m != 0) break;
+    if (__builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_DONE])) >= P.chains) return -1;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > MIG_WAIT_TICKS) {
+      int still = 0;   // withdraw the post unless a donor already claimed it
+      if (lane == 0) {
+        still = (g_and(&M.fmask[me], ~(1 << c)) >> c) & 1;
+        if (still) g_add(&M.hdr[MIG_WAITING], -1);
+      }
+      if (__shfl(still, 0)) return -1;
+      while ((m = __builtin_amdgcn_readfirstlane(g_load_acq(box))) == 0) __builtin_amdgcn_s_sleep(8);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(32);
+  }
+  if (lane == 0) g_store_rel(box, 0);
+  const AS_GLB double* src =
+      (const AS_GLB double*)P.mig_img + (size_t)(me * GMAX + c) * P.mig_img_words;
+  AS_LDS double* dst = (AS_LDS double*)L.chain(c);
+  for (int i = lane; i < P.mig_img_words; i += WAVE) dst[i] = src[i];
+  wave_fence();
+  return m - 1;
+}
+
 // Dataflow pipeline inside a tile.  The NUTS wave of chain c writes the next
 // position's parameters to MP[c] and enqueues c in an LDS ring (64-bit entries
 // {sequence number, chain}); the gradient waves drain the ring in order, each
@@ -1578,6 +1715,15 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     start_max[tid] = 0;
   }
   if (tid < RINGN) ring[tid] = ~0ULL;
+  if (P.mig != nullptr) {   // every slot of the tile may host migrants: all NUTS waves live
+    if (tid == 0) {
+      const MigView M(P.mig, P.mig_tiles);
+      n_active = P.G;
+      __hip_atomic_store((int*)&M.load[blockIdx.x], nct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add((int*)&M.hdr[MIG_STARTED], 1, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   __syncthreads();
 
   const bool stamp = kProfile && (P.stamps != nullptr) && lane == 0 && (wave == 0 || wave == NGW);
@@ -1590,6 +1736,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     Bins<R, BPT, NNP, MODE> bins;
     bins.load(P, tid);
     int zero_done[GMAX] = {0, 0, 0, 0};
+    unsigned long long t_idle = 0;
     for (unsigned h = 0;; ++h) {
       unsigned long long e;
       bool stop = false;
@@ -1597,9 +1744,23 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       for (;;) {  // wait for ring entry h
         e = lds_load64(&ring[h % RINGN]);
         if ((unsigned)(e >> 32) == h) break;
-        if (lds_load(&n_active) == 0 || ++spins > SPIN_LIMIT) {
+        if (lds_load(&n_active) == 0) {
           stop = true;
           break;
+        }
+        // hang guard: with migration a tile may idle (receivers posted) until
+        // the launch's last chain ends, so the bound is in time, not polls
+        if (++spins > SPIN_LIMIT) {
+          if (P.mig == nullptr) {
+            stop = true;
+            break;
+          }
+          if (spins == SPIN_LIMIT + 1) t_idle = __builtin_amdgcn_s_memrealtime();
+          if (__builtin_amdgcn_s_memrealtime() - t_idle > MIG_WAIT_TICKS + 1000000000ULL) {
+            stop = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(32);
         }
         __builtin_amdgcn_s_sleep(1);
       }
@@ -1632,14 +1793,19 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     // throughput-bound gradient waves: let it win issue arbitration
     __builtin_amdgcn_s_setprio(3);
     const int c = wave - NGW;
-    if (c < nct) {
+    const bool mig = P.mig != nullptr;
+    if (c < (mig ? P.G : nct)) {
       using Ch = Chain<PPL, NNP, FAM>;
-      Ch ch(P, L, c, c0 + c, lane, nct);
-      long long epoch = 0;
+      long long epoch = 0;     // this slot's hand-offs (grad_cnt[c] counts NGW per epoch)
+      int lc = c < nct ? c0 + c : -1;
       int a = Ch::A_INIT_STATE;
-      bool in_sweep = false;   // the last run() was A_PRIOR, overlapping the chain's sweep
-      // ONE call site of the action machine (it is inlined once, not per caller)
-      for (;;) {
+      for (;;) {   // the slot's own chain, then (migration) chains handed over by other tiles
+       if (lc >= 0) {
+        Ch ch(P, L, c, lc, lane, nct);
+        long long steps = 0;
+        bool in_sweep = false;   // the last run() was A_PRIOR, overlapping the chain's sweep
+        // ONE call site of the action machine (it is inlined once, not per caller)
+        for (;;) {
         const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
         ch.run(a);
         if (in_sweep) {
@@ -1672,8 +1838,9 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           t_busy += (long long)__builtin_amdgcn_s_memtime() - s0;
           ++n_items;
         }
-        if (ch.Sp->state == ST_DONE) break;
-        if (epoch >= P.max_steps) {   // termination guarantee: report, never hang
+        const int stt = __builtin_amdgcn_readfirstlane(ch.Sp->state);
+        if (stt == ST_DONE || stt == ST_MOVED) break;
+        if (++steps > P.max_steps) {   // termination guarantee: report, never hang
           ch.Sp->status = ERR_TIMEOUT;
           a = Ch::A_FINISH;
           continue;
@@ -1689,6 +1856,18 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         // position-only work (prior terms, next merges' uniforms) overlaps the sweep
         a = Ch::A_PRIOR;
         in_sweep = true;
+        }
+        if (mig && lane == 0 && __builtin_amdgcn_readfirstlane(ch.Sp->state) == ST_DONE) {
+          const MigView M(P.mig, P.mig_tiles);
+          g_add(&M.load[blockIdx.x], -1);
+          __hip_atomic_fetch_add((int*)&M.hdr[MIG_DONE], 1, __ATOMIC_RELEASE,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        }
+       }
+        if (!mig) break;
+        lc = receive_chain<PPL>(P, L, c, lane);
+        if (lc < 0) break;
+        a = Ch::A_START_TRANSITION;
       }
       wave_fence();
       if (lane == 0) atomicSub(&n_active, 1);
@@ -1785,6 +1964,10 @@ __global__ void __launch_bounds__(TPB, 2) logp_kernel(const KParams* __restrict_
 #if FITOCT_FAMILY == 0
 int lds_bytes(int ppl, int G, int max_depth) {
   return ppl == 1 ? Lds<1>::bytes(G, max_depth) : Lds<2>::bytes(G, max_depth);
+}
+// doubles in a chain's migration image: its LDS region up to the tree levels
+int mig_img_words(int ppl) {
+  return ppl == 1 ? Lds<1>::chain_bytes(0) / 8 : Lds<2>::chain_bytes(0) / 8;
 }
 #endif
 

@@ -114,7 +114,7 @@ typedef struct fitoct_result {
   int32_t n_cols;           /* out */
   int32_t iters_saved;      /* out */
   int32_t dim;              /* out: D, unconstrained dimension */
-  int32_t pad_;
+  int32_t migrations;       /* out: chains handed between tiles (work balance; no effect on draws) */
   int64_t total_leapfrogs;  /* out: sum of n_leapfrog__ over every transition of every chain */
   double kernel_ms;         /* out: device time of the sampler kernel (HIP events) */
   double wall_ms;           /* out: host wall time of the call */
