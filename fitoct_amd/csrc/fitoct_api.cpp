@@ -54,7 +54,7 @@ struct fitoct_plan {
   fitoct_problem prob{};
   fitoct_config cfg{};
   KParams kp{};
-  int tiles = 0, bpt = 0, nnp = 16, ppl = 1, lds = 0, ncu = 0;
+  int tiles = 0, bpt = 0, nnp = 15, ppl = 1, lds = 0, ncu = 0;
   bool mixed = false;
   int* d_mig = nullptr;       // chain-migration control block (see MigCtrl)
   double* d_mig_img = nullptr;
@@ -295,9 +295,11 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   pl->prob.x = pl->prob.y = pl->prob.uy = pl->prob.B = nullptr;  // never keep caller pointers
   pl->mixed = (precision == FITOCT_PREC_MIXED);
   const int D = model_dim(p->prior_type, p->Nn);
-  pl->nnp = (p->Nn <= 16) ? 16 : 24;
+  // NNP: padded control-point count of the kernel instantiation (15 = FitOCT's Nn,
+  // ctrlParams.yaml:4, with no padding work in the sweep; 24 covers Nn = 16..24)
+  pl->nnp = (p->Nn <= 15) ? 15 : 24;
   pl->ppl = (D <= WAVE) ? 1 : 2;
-  if (pl->nnp == 16 && pl->ppl == 2) pl->nnp = 24;  // the (24, 2) instantiation covers it
+  if (pl->nnp == 15 && pl->ppl == 2) pl->nnp = 24;  // the (24, 2) instantiation covers it
   if (pl->nnp == 24) pl->ppl = 2;
   const bool mono = p->prior_type == FITOCT_MODEL_MONOEXP;
   std::vector<double> B, xg;

@@ -293,21 +293,25 @@ __device__ __forceinline__ void normal_pair(RngKey k, uint32_t c0, uint32_t c1, 
 // ---------------------------------------------------------------------------
 template <class R> __device__ __forceinline__ R rcp_(R x);
 template <> __device__ __forceinline__ double rcp_<double>(double x) {
-  double r = __builtin_amdgcn_rcp(x);          // ~2^-26 seed
-  double e = fma(-x, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-x, r, 1.0);
-  return fma(r, e, r);   // 2 Newton steps: 0 ulp from 1/x over 4M samples (scripts/micro/acc.hip)
+  const double r = __builtin_amdgcn_rcp(x);    // v_rcp_f64 (quarter rate)
+  const double e = fma(-x, r, 1.0);
+  return fma(r, e, r);   // one Newton step: <= 1 ulp from 1/x (scripts/micro/acc.hip)
 }
 template <> __device__ __forceinline__ float rcp_<float>(float x) {
   return __builtin_amdgcn_rcpf(x);
 }
 template <class R> __device__ __forceinline__ R exp_(R x);
 // exp for the sweep: reduction by ln2 (hi/lo), Taylor degree 12 on |r| <= ln2/2,
-// ldexp.  <= 2 ulp from the library exp on [-700, 0] (scripts/micro/acc.hip) and
-// no special-case selects: arguments here are <= 0, underflow ends in 0 via ldexp.
+// ldexp.  n = round(x log2 e) comes from the 1.5*2^52 shifter (its low word is n
+// as an int, fed straight to v_ldexp_f64: no v_rndne / v_cvt_i32_f64, the latter
+// half rate).  x is clamped at -746 (below it exp is 0 either way, and the shifter
+// needs |x log2 e| < 2^51); arguments here are <= 0, underflow ends in 0 via ldexp.
 template <> __device__ __forceinline__ double exp_<double>(double x) {
-  const double n = rint(x * 1.4426950408889634);
+  x = fmax(x, -746.0);
+  const double SH = 6755399441055744.0;   // 1.5 * 2^52
+  const double t = fma(x, 1.4426950408889634, SH);
+  const double n = t - SH;
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
   double r = fma(-n, 6.93147180369123816490e-01, x);
   r = fma(-n, 1.90821492927058770002e-10, r);
   double p = 2.08767569878680989792e-09;   // 1/12!
@@ -323,15 +327,19 @@ template <> __device__ __forceinline__ double exp_<double>(double x) {
   p = fma(p, r, 0.5);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
-  return ldexp(p, (int)n);
+  return ldexp(p, ni);
 }
 template <> __device__ __forceinline__ float exp_<float>(float x) { return __expf(x); }
 
 // Likelihood terms of one bin given its modulation dL (shared by every mode).
 // acc: [0] sum d^2, [1] sum a, [2] sum a e, [3] sum w; returns h (adjoint seed of dL).
+// The non-physical guard (1 + dL <= 0 -> lp = -inf) is a per-lane running min
+// (umin), applied once after the lane's bins (no per-bin selects).
 template <class R, class A, int NA>
-__device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th3, A (&acc)[NA]) {
+__device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th3, A (&acc)[NA],
+                                      R& umin) {
   const R u = R(1) + dL;
+  umin = fmin(umin, u);
   const R L = th3 * u;                                           // decay length theta3*(1+dL)
   const R iL = rcp_<R>(L);
   const R e = exp_<R>(-cx * iL);                                 // exp(-c x / L)
@@ -344,18 +352,17 @@ __device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th
   acc[1] += (A)a;
   acc[2] += (A)ae;
   acc[3] += (A)w;
-  if (!(u > R(0))) acc[0] = (A)INFINITY;                         // non-physical decay length
   return w * iL;                                                 // dlp/ddL / (th2 th3) * sigma^2
 }
 
 // MODE_POLY: dL = a P(t) with P = sum_l c_l t^l ; moments M_l += h a t^l
 template <class R, int NNP, class A>
 __device__ __forceinline__ void bin_poly(R cx, R y, R isu, R t, R av, R th1, R th2, R th3,
-                                         const R (&cf)[NNP], A (&acc)[4 + NNP]) {
+                                         const R (&cf)[NNP], A (&acc)[4 + NNP], R& umin) {
   R P = cf[NNP - 1];
 #pragma unroll
   for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
-  const R h = bin_core<R, A, 4 + NNP>(av * P, cx, y, isu, th1, th2, th3, acc);
+  const R h = bin_core<R, A, 4 + NNP>(av * P, cx, y, isu, th1, th2, th3, acc, umin);
   R p = h * av;
   acc[4] += (A)p;
 #pragma unroll
@@ -369,11 +376,11 @@ __device__ __forceinline__ void bin_poly(R cx, R y, R isu, R t, R av, R th1, R t
 // the bin's weight in the moments (accumulated per lane by moments_geo).
 template <class R, int NNP, class A>
 __device__ __forceinline__ R bin_poly_fwd(R cx, R y, R isu, R t, R av, R th1, R th2, R th3,
-                                          const R (&cf)[NNP], A (&acc)[4 + NNP]) {
+                                          const R (&cf)[NNP], A (&acc)[4 + NNP], R& umin) {
   R P = cf[NNP - 1];
 #pragma unroll
   for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
-  return bin_core<R, A, 4 + NNP>(av * P, cx, y, isu, th1, th2, th3, acc) * av;
+  return bin_core<R, A, 4 + NNP>(av * P, cx, y, isu, th1, th2, th3, acc, umin) * av;
 }
 
 // Moments of one lane's BPT bins t_b = t0 R^b:  M_l = t0^l sum_b w_b (R^l)^b.
@@ -396,11 +403,11 @@ __device__ __forceinline__ void moments_geo(KPc& P, double t0, const double (&w)
 // MODE_ROWS / MODE_STREAM: dL = B_i . yGP ; (B^T h)_k += B_ik h
 template <class R, int NNP, class A>
 __device__ __forceinline__ void bin_rows(R cx, R y, R isu, const R (&Brow)[NNP], R th1, R th2,
-                                         R th3, const R (&yg)[NNP], A (&acc)[4 + NNP]) {
+                                         R th3, const R (&yg)[NNP], A (&acc)[4 + NNP], R& umin) {
   R dL = R(0);
 #pragma unroll
   for (int k = 0; k < NNP; ++k) dL = fma(Brow[k], yg[k], dL);
-  const R h = bin_core<R, A, 4 + NNP>(dL, cx, y, isu, th1, th2, th3, acc);
+  const R h = bin_core<R, A, 4 + NNP>(dL, cx, y, isu, th1, th2, th3, acc, umin);
 #pragma unroll
   for (int k = 0; k < NNP; ++k) acc[4 + k] = fma((A)Brow[k], (A)h, acc[4 + k]);
 }
@@ -555,25 +562,26 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
     double acc[4 + NNP];
 #pragma unroll
     for (int k = 0; k < 4 + NNP; ++k) acc[k] = 0.0;
+    R umin = R(1);
     if constexpr (BPT > 0 && MODE == MODE_POLY && sizeof(R) == 8) {
       if (P.geo) {
         double w[BPT];
 #pragma unroll
         for (int b = 0; b < BPT; ++b)
           w[b] = bin_poly_fwd<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
-                                              bins.row[b][1], th1, th2, th3, cf, acc);
+                                              bins.row[b][1], th1, th2, th3, cf, acc, umin);
         moments_geo<BPT, NNP>(P, bins.row[0][0], w, acc);
       } else {
 #pragma unroll
         for (int b = 0; b < BPT; ++b)
           bin_poly<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
-                                   bins.row[b][1], th1, th2, th3, cf, acc);
+                                   bins.row[b][1], th1, th2, th3, cf, acc, umin);
       }
     } else if constexpr (BPT > 0 && MODE == MODE_POLY) {
 #pragma unroll
       for (int b = 0; b < BPT; ++b)
         bin_poly<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
-                                 bins.row[b][1], th1, th2, th3, cf, acc);
+                                 bins.row[b][1], th1, th2, th3, cf, acc, umin);
     } else if constexpr (BPT > 0) {
       // the few bins of one lane accumulate in R, the lane totals in f64
       R racc[4 + NNP];
@@ -582,7 +590,7 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
 #pragma unroll
       for (int b = 0; b < BPT; ++b)
         bin_rows<R, NNP, R>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b], th1, th2, th3, cf,
-                            racc);
+                            racc, umin);
 #pragma unroll
       for (int k = 0; k < 4 + NNP; ++k) acc[k] = (double)racc[k];
     } else {
@@ -593,15 +601,16 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
       for (int i = tid; i < P.n_pad; i += GT) {
         if constexpr (MODE == MODE_POLY) {
           bin_poly<R, NNP, double>(pcx[i], py[i], pisu[i], pB[2 * (size_t)i], pB[2 * (size_t)i + 1],
-                                   th1, th2, th3, cf, acc);
+                                   th1, th2, th3, cf, acc, umin);
         } else {
           R row[NNP];
 #pragma unroll
           for (int k = 0; k < NNP; ++k) row[k] = pB[(size_t)i * NNP + k];
-          bin_rows<R, NNP, double>(pcx[i], py[i], pisu[i], row, th1, th2, th3, cf, acc);
+          bin_rows<R, NNP, double>(pcx[i], py[i], pisu[i], row, th1, th2, th3, cf, acc, umin);
         }
       }
     }
+    if (!(umin > R(0))) acc[0] = INFINITY;   // some bin has 1 + dL <= 0: lp = -inf
     int idx;
     const double r = transpose_reduce<4 + NNP>(acc, lane, idx);
     if (!(lane & 1) && idx >= 0) part[(c * NGW + wave) * NSLOT + idx] = r;
@@ -762,10 +771,11 @@ struct Chain {
       if (lane < NNP) {
         double c0 = 0.0, c1 = 0.0;   // two chains of FMAs: half the dependent latency
 #pragma unroll
-        for (int k = 0; k < NNP; k += 2) {
+        for (int k = 0; k + 1 < NNP; k += 2) {
           c0 = fma(Kinv[lane * NNP + k], AUX[k], c0);
           c1 = fma(Kinv[lane * NNP + k + 1], AUX[k + 1], c1);
         }
+        if constexpr ((NNP & 1) != 0) c0 = fma(Kinv[lane * NNP + NNP - 1], AUX[NNP - 1], c0);
         MP[4 + lane] = (c0 + c1) * bv[lane];
       }
     }
@@ -2020,9 +2030,9 @@ hipError_t FITOCT_CAT(launch_family_, FITOCT_FAMILY)(bool logp, bool mixed, int 
                                                      int tiles, hipStream_t st,
                                                      const int* tile_map) {
 #ifdef FITOCT_ONE_VARIANT
-  return launch_t<double, 8, 16, 1, MODE_POLY>(logp, P, dP, tiles, st, tile_map);
+  return launch_t<double, 8, 15, 1, MODE_POLY>(logp, P, dP, tiles, st, tile_map);
 #else
-  if (nnp == 16) return launch_n<16, 1>(logp, mixed, bpt, P, dP, tiles, st, tile_map);
+  if (nnp == 15) return launch_n<15, 1>(logp, mixed, bpt, P, dP, tiles, st, tile_map);
   return launch_n<24, 2>(logp, mixed, bpt, P, dP, tiles, st, tile_map);
 #endif
 }
