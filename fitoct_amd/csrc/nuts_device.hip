@@ -913,10 +913,11 @@ struct Chain {
         if (poly) {
           double v1 = 0.0;
 #pragma unroll
-          for (int m = 0; m < NNP; m += 2) {
+          for (int m = 0; m + 1 < NNP; m += 2) {
             v = fma(Kinv[lane * NNP + m], SUMS[4 + m], v);
             v1 = fma(Kinv[lane * NNP + m + 1], SUMS[4 + m + 1], v1);
           }
+          if constexpr ((NNP & 1) != 0) v = fma(Kinv[lane * NNP + NNP - 1], SUMS[4 + NNP - 1], v);
           v += v1;
           SUMS[4 + lane] = v;   // every lane's reads above precede this store
         } else {
@@ -1618,9 +1619,9 @@ template <int PPL, int NNP>
 __device__ __forceinline__ void load_kinv(KPc& P, const Lds<PPL>& L, int tid) {
   if (P.mode == MODE_POLY) {  // zero-padded to NNP x NNP so the device loops are fixed-size
     const int Nn = P.Nn;
-    for (int i = tid; i < NNP * NNP; i += TPB) {
+    for (int i = tid; i < KMAX * KMAX; i += TPB) {   // whole tile: no stale LDS is ever read
       const int r = i / NNP, c = i % NNP;
-      L.kinv()[i] = (r < Nn && c < Nn) ? P.Kinv[r * Nn + c] : 0.0;
+      L.kinv()[i] = (i < NNP * NNP && r < Nn && c < Nn) ? P.Kinv[r * Nn + c] : 0.0;
     }
     if (tid < NNP) L.bv()[tid] = (tid < Nn) ? P.bvec[tid] : 0.0;
   }
