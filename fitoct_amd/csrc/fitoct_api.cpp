@@ -251,7 +251,13 @@ bool geo_ratios(const fitoct_problem* p, int nnp, int bpt, double* R) {
                                                            : 1.0 / (Nn - 1);
   const double logR = GT * (step / range) * dg / s2;
   if (fabs(logR) * (nnp - 1) * (bpt - 1) > 600.0) return false;
-  for (int l = 0; l < nnp; ++l) R[l] = exp(l * logR);
+  if (bpt == 16) {   // c*x_b and t_b are formed in the kernel: x must be on the line to ~ulps
+    for (int i = 0; i < N; ++i)
+      if (fabs(p->x[i] - (p->x[0] + i * step)) > 4e-16 * std::max(fabs(xmin), fabs(xmax)) + 1e-300)
+        return false;
+    if (fabs(logR) * (bpt - 1) > 600.0) return false;
+  }
+  for (int l = 0; l < 24; ++l) R[l] = exp(l * logR);
   return true;
 }
 
@@ -327,6 +333,15 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   // f64 rows (NNP doubles per bin) are always streamed
   int n_pad;
   choose_bins(p->N, mode == MODE_POLY ? 8 : pl->mixed ? 4 : 0, pl->bpt, n_pad);
+  // N in (2048, 4096] on an arithmetic depth grid: 16 bins per lane in the compact
+  // layout (y, 1/uy, a in registers; c*x and t formed from the lane's first bin)
+  double R16[24];
+  if (mode == MODE_POLY && !mono && !pl->mixed && pl->bpt == 0 && p->N <= 16 * GT &&
+      force_bpt < 0 && getenv("FITOCT_NO_GEO") == nullptr && getenv("FITOCT_NO_BPT16") == nullptr &&
+      geo_ratios(p, pl->nnp, 16, R16)) {
+    pl->bpt = 16;
+    n_pad = 16 * GT;
+  }
   if (force_bpt >= 0 && force_bpt != pl->bpt) {   // batch: the batch's common bin layout
     if (force_bpt != 0 && force_bpt < pl->bpt) return fail(FITOCT_E_ARG, "bin layout too small");
     pl->bpt = force_bpt;
@@ -357,6 +372,13 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   k.n_pad = n_pad;
   k.geo = (mode == MODE_POLY && !mono && !pl->mixed && getenv("FITOCT_NO_GEO") == nullptr)
               ? geo_ratios(p, pl->nnp, pl->bpt, k.geo_R) : 0;
+  if (pl->bpt == 16) {
+    if (!k.geo) return fail(FITOCT_E_INTERNAL, "16-bin layout without a geometric grid");
+    const double cstep = (double)p->data_type * (p->x[p->N - 1] - p->x[0]) / (p->N - 1);
+    for (int b = 0; b < 16; ++b) k.geo_dcx[b] = (double)b * GT * cstep;
+    k.geo_tmax = 0.0;
+    for (int i = 0; i < p->N; ++i) k.geo_tmax = std::max(k.geo_tmax, ta[2 * (size_t)i]);
+  }
   k.Nn = mono ? 0 : p->Nn;
   k.D = D;
   k.family = p->prior_type;

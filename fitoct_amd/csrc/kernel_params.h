@@ -54,7 +54,12 @@ struct KParams {
   // POLY on a uniform depth grid: bin tid + b*GT has t = t_tid * R^b, so a lane's
   // moments sum_b w_b t_b^l = t_tid^l * sum_b w_b (R^l)^b (Horner in R^l).
   int geo;                  // 1: geo_R valid (host-verified arithmetic x grid)
-  double geo_R[24];         // R^l, l < NNP
+  double geo_R[24];         // R^l, l < 24 (moments: l < NNP; BPT 16 also t_b = t_tid R^b)
+  // BPT == 16 (N in (2048, 4096] on an arithmetic grid): a lane keeps only y, 1/uy
+  // and a of its 16 bins; c*x_b = cx_tid + geo_dcx[b] and t_b = min(t_tid R^b, geo_tmax)
+  // (the clamp keeps padding bins, whose a is 0, finite)
+  double geo_dcx[16];
+  double geo_tmax;
   double theta0[3];
   double S0inv[9];
   double lambda_rate_eff;   // rate of the exponential prior on lambda (normal family)

@@ -400,6 +400,22 @@ __device__ __forceinline__ void moments_geo(KPc& P, double t0, const double (&w)
   }
 }
 
+// The same for one 8-bin half of a 16-bin lane (BPT 16): M_l += t0^l sum_b w_b (R^l)^b.
+template <int NB, int NNP>
+__device__ __forceinline__ void moments_geo_add(KPc& P, double t0, const double (&w)[NB],
+                                                double (&acc)[4 + NNP]) {
+  double pw = 1.0;
+#pragma unroll
+  for (int l = 0; l < NNP; ++l) {
+    const double X = P.geo_R[l];
+    double S = w[NB - 1];
+#pragma unroll
+    for (int b = NB - 2; b >= 0; --b) S = fma(S, X, w[b]);
+    acc[4 + l] = fma(pw, S, acc[4 + l]);
+    pw *= t0;
+  }
+}
+
 // MODE_ROWS / MODE_STREAM: dL = B_i . yGP ; (B^T h)_k += B_ik h
 template <class R, int NNP, class A>
 __device__ __forceinline__ void bin_rows(R cx, R y, R isu, const R (&Brow)[NNP], R th1, R th2,
@@ -500,14 +516,26 @@ struct Bins {
       const AS_GLB R* py = (const AS_GLB R*)P.y;
       const AS_GLB R* pisu = (const AS_GLB R*)P.isu;
       const AS_GLB R* pB = (const AS_GLB R*)P.B;
+      if constexpr (BPT == 16) {   // compact: y, 1/uy, a per bin; c*x and t of bin 0 only
+        cx[0] = pcx[tid];
+        row[0][0] = pB[2 * (size_t)tid];
 #pragma unroll
-      for (int b = 0; b < BPT; ++b) {
-        const int i = tid + b * GT;
-        cx[b] = pcx[i];
-        y[b] = py[i];
-        isu[b] = pisu[i];
+        for (int b = 0; b < BPT; ++b) {
+          const int i = tid + b * GT;
+          y[b] = py[i];
+          isu[b] = pisu[i];
+          row[b][1] = pB[2 * (size_t)i + 1];
+        }
+      } else {
 #pragma unroll
-        for (int k = 0; k < NR; ++k) row[b][k] = pB[(size_t)i * NR + k];
+        for (int b = 0; b < BPT; ++b) {
+          const int i = tid + b * GT;
+          cx[b] = pcx[i];
+          y[b] = py[i];
+          isu[b] = pisu[i];
+#pragma unroll
+          for (int k = 0; k < NR; ++k) row[b][k] = pB[(size_t)i * NR + k];
+        }
       }
     }
   }
@@ -563,7 +591,22 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
 #pragma unroll
     for (int k = 0; k < 4 + NNP; ++k) acc[k] = 0.0;
     R umin = R(1);
-    if constexpr (BPT > 0 && MODE == MODE_POLY && sizeof(R) == 8) {
+    if constexpr (BPT == 16) {   // MODE_POLY f64 on an arithmetic grid (host-checked)
+      const double cx0 = bins.cx[0], t0 = bins.row[0][0], tmax = P.geo_tmax;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        double w[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const int bb = half * 8 + b;
+          const double cxb = cx0 + P.geo_dcx[bb];
+          const double tb = fmin(t0 * P.geo_R[bb], tmax);
+          w[b] = bin_poly_fwd<R, NNP, double>(cxb, bins.y[bb], bins.isu[bb], tb,
+                                              bins.row[bb][1], th1, th2, th3, cf, acc, umin);
+        }
+        moments_geo_add<8, NNP>(P, half ? t0 * P.geo_R[8] : t0, w, acc);
+      }
+    } else if constexpr (BPT > 0 && MODE == MODE_POLY && sizeof(R) == 8) {
       if (P.geo) {
         double w[BPT];
 #pragma unroll
@@ -2009,6 +2052,10 @@ static hipError_t launch_m(bool logp, int bpt, const KParams& P, const KParams* 
     case 4: return launch_t<R, 4, NNP, PPL, MODE>(logp, P, dP, tiles, st, tm);
     case 8:
       if constexpr (MODE == MODE_POLY) return launch_t<R, 8, NNP, PPL, MODE>(logp, P, dP, tiles, st, tm);
+      return hipErrorInvalidValue;
+    case 16:   // compact geo layout, f64 only (N in (2048, 4096] on an arithmetic grid)
+      if constexpr (MODE == MODE_POLY && sizeof(R) == 8)
+        return launch_t<R, 16, NNP, PPL, MODE>(logp, P, dP, tiles, st, tm);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }

@@ -66,7 +66,9 @@ CASES = [
     (481, "horseshoe", 10, "internal", 1, 2, 0, 0),     # prior predictive (priPost.R:14)
     (700, "horseshoe", 20, "internal", 0, 1, 1, 1),     # amplitude data, RMgauss, rate conv
     (2047, "lasso", 5, "internal", 0, 2, 0, 0),         # ragged
-    (8192, "normal", 15, "extremal", 0, 2, 0, 0),       # > 2048 bins: streamed from HBM
+    (8192, "normal", 15, "extremal", 0, 2, 0, 0),       # > 4096 bins: streamed from HBM
+    (3001, "horseshoe", 15, "extremal", 0, 2, 0, 0),    # 16 bins per lane, padded
+    (2049, "normal", 15, "internal", 0, 1, 0, 0),       # 16 bins per lane, mostly padding
     (2, "normal", 2, "extremal", 0, 2, 0, 0),           # minimum shape
     (97, "horseshoe", 24, "extremal", 0, 2, 0, 0),      # maximum Nn
     (1025, "normal", 8, "internal", 0, 2, 0, 0),        # just over a bins-per-thread step

@@ -64,7 +64,8 @@ def test_reproduces_oracle_draw_fixture(path):
 
 CASES = [("normal", 256, 10, 150, 100), ("horseshoe", 300, 8, 150, 100),
          ("lasso", 200, 12, 100, 100), ("normal", 1000, 15, 150, 60),
-         ("horseshoe", 2048, 15, 100, 40)]
+         ("horseshoe", 2048, 15, 100, 40),
+         ("lasso", 3001, 15, 100, 40)]   # 16 bins per lane (compact layout) with padding
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}-N{c[1]}")
