@@ -44,7 +44,7 @@ CONFIGS = {
     4: dict(prior="lasso", N=4096, chains=1024),
     # FitOCT.R batch mode: 256 synthetic files (the 4 modulations of synthData.R:21,35,49,
     # 63 at N=481), 4 chains each, ctrlParams.yaml's 100 warmup + 100 draws, Nn=15
-    # extremal, normal prior; files sharded round-robin over the ranks (strong scaling)
+    # extremal, normal prior; files sharded in contiguous blocks over the ranks (strong scaling)
     5: dict(prior="normal", N=481, chains=4, files=256, iters=(100, 100)),
 }
 FP64_VALU_PEAK_TF = 78.6          # MI355X FP64 vector peak (vendor spec; 1/2 of FP32 vector)
@@ -291,7 +291,9 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
 
     conf = CONFIGS[5]
     t0, S0 = default_prior()
-    files = list(range(rank, conf["files"], world))     # round-robin by file
+    from fitoct_amd.distributed import shard_range
+    f_off, f_cnt = shard_range(conf["files"], world, rank)   # contiguous file blocks
+    files = list(range(f_off, f_off + f_cnt))
     probs = []
     for f in files:
         d = synth_decay(conf["N"], MODULATIONS[f % 4], 1234 + f)
@@ -301,8 +303,10 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
     C = args.chains or conf["chains"]
 
     def batch_for(step):
+        # file f's chains are global chains f*C + c (fitoct_amd.distributed.sample_batch_sharded)
         cfg = SamplerConfig(chains=C, warmup=W_it, samples=S_it, seed=2000 + step,
-                            adapt_delta=0.8, max_treedepth=10, device=local)
+                            adapt_delta=0.8, max_treedepth=10, device=local,
+                            chain_offset=f_off * C)
         return Batch(probs, cfg)
 
     stream = torch.cuda.current_stream(dev)
@@ -366,7 +370,7 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
         "config": {"workload": f"FitOCT.R batch: {conf['files']} files x {C} chains, "
                                f"fitExpGP+{conf['prior']} N={conf['N']} Nn={NN} W={W_it} S={S_it}",
                    "files": conf["files"], "files_this_rank": len(files), "chains_per_file": C,
-                   "parallelism": f"files round-robin over {world} GPU(s), one launch per GPU"},
+                   "parallelism": f"files in contiguous blocks over {world} GPU(s), one launch per GPU"},
         "rhat_max_median_file": round(float(np.median(rh_file)), 4),
         "rhat_max_worst_file": round(float(np.max(rh_file)), 4),
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TF,

@@ -407,6 +407,7 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
     return fail(FITOCT_E_ARG, "max_treedepth too large for the LDS budget");
   k.G = G;
   k.max_depth = max_depth;
+  k.nuts_prio = getenv("FITOCT_NUTS_PRIO") ? atoi(getenv("FITOCT_NUTS_PRIO")) : 3;
   pl->tiles = (chains + G - 1) / G;
   pl->lds = lds_bytes(pl->ppl, G, max_depth);
   return FITOCT_OK;
@@ -958,16 +959,23 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
     // bins: every tile runs the batch's widest bin layout.  A problem planned with
     // fewer bins per lane is restaged at the common n_pad (zero-weight padding).
     if (bpt == 1 << 20) bpt = 0;
-    for (size_t p = 0; p < b->plans.size(); ++p) {
-      fitoct_plan* pl = b->plans[p];
-      if (pl->bpt == bpt) continue;
-      fitoct_config c = *cfg;
-      c.chain_offset = cfg->chain_offset + (int)p * C;
-      free_plan(pl);
-      b->plans[p] = nullptr;
-      const int rc = plan_create(&probs[p], &c, n_problems * C, bpt, &b->plans[p]);
-      if (rc) return rc;
-    }
+    auto restage = [&](int to) -> int {
+      for (size_t p = 0; p < b->plans.size(); ++p) {
+        fitoct_plan* pl = b->plans[p];
+        if (pl && pl->bpt == to) continue;
+        fitoct_config c = *cfg;
+        c.chain_offset = cfg->chain_offset + (int)p * C;
+        free_plan(pl);
+        b->plans[p] = nullptr;
+        const int rc = plan_create(&probs[p], &c, n_problems * C, to, &b->plans[p]);
+        if (rc) return rc;
+      }
+      return FITOCT_OK;
+    };
+    int rc = restage(bpt);
+    // the 16-bin layout needs an arithmetic depth grid in every problem: else stream all
+    if (rc && bpt == 16) rc = restage(0);
+    if (rc) return rc;
     b->per_bytes = b->plans[0]->draws_bytes;
     std::vector<int> map;
     const int G = b->plans[0]->kp.G;

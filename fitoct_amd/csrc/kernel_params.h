@@ -89,6 +89,7 @@ struct KParams {
   int* mig;                 // MigCtrl header | load | free_mask | mailbox (see MigCtrl)
   double* mig_img;          // [tiles * GMAX][mig_img_words] chain images in flight
   int mig_tiles, mig_img_words;
+  int nuts_prio;            // s_setprio of the NUTS waves (0..3)
   // ---- logp mode ----
   const double* q_in;       // [points][D]
   double* lp_out;           // [points]

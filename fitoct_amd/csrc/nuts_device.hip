@@ -69,6 +69,13 @@ enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2, FAM_MONO = 3 };
 #define FITOCT_PROFILE 0
 #endif
 constexpr bool kProfile = FITOCT_PROFILE != 0;
+// -DFITOCT_ASM_MARKS: assembly comments at action boundaries, for per-action
+// instruction counts in a -S listing (scripts/asm_actions.py); no code otherwise
+#ifdef FITOCT_ASM_MARKS
+#define FITOCT_MARK(name) asm volatile(";MARK " #name)
+#else
+#define FITOCT_MARK(name)
+#endif
 enum { ERR_INIT = -4, ERR_NUMERIC = -5, ERR_TIMEOUT = -6 };
 
 // vectors kept in LDS per chain (lane-private elements)
@@ -580,6 +587,7 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                               const AS_LDS double* mpall, AS_LDS double* part, const int* done,
                               int cb, int ce,
                               int tid, int lane, int wave) {
+  FITOCT_MARK(gradient_pass);
   for (int c = cb; c < ce; ++c) {
     if (done[c]) continue;   // wave-uniform (LDS broadcast)
     const AS_LDS double* mp = mpall + c * MPW;
@@ -655,6 +663,7 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
     }
     if (!(umin > R(0))) acc[0] = INFINITY;   // some bin has 1 + dL <= 0: lp = -inf
     int idx;
+    FITOCT_MARK(sweep_reduce);
     const double r = transpose_reduce<4 + NNP>(acc, lane, idx);
     if (!(lane & 1) && idx >= 0) part[(c * NGW + wave) * NSLOT + idx] = r;
   }
@@ -776,6 +785,8 @@ struct Chain {
   // theta[3] and, per basis mode, yGP (rows) or c = b .* K^-1 yGP (poly).
   // (LDS exchange: on gfx950 a v_readlane assembly of yGP measured 3x slower.)
   __device__ void write_mp(const V& q) const {
+    FITOCT_MARK(write_mp);
+    long long ts = stamp0();
     const int Nn = Pr().Nn, D = Pr().D;
     const bool poly = Pr().mode == MODE_POLY;
     AS_LDS double* qs = vec(V_QS);
@@ -809,6 +820,7 @@ struct Chain {
       AUX[32 + lane] = hl;
       if (!poly) MP[4 + lane] = yv;
     }
+    sub(5, ts);
     if (poly) {  // c_l = b_l (K^-1 yGP)_l ; K^-1 padded to NNP x NNP
       wave_fence();
       if (lane < NNP) {
@@ -822,6 +834,7 @@ struct Chain {
         MP[4 + lane] = (c0 + c1) * bv[lane];
       }
     }
+    sub(6, ts);
   }
 
   // The lp / grad completion is split so that everything depending only on the
@@ -840,6 +853,7 @@ struct Chain {
   }
 
   __device__ void prior_part() const {
+    FITOCT_MARK(prior_part);
     const int D = Pr().D, Nn = Pr().Nn;
     constexpr int fam = FAM;
     const AS_LDS double* qs = QS();
@@ -935,6 +949,7 @@ struct Chain {
   // trips: bin sums out (-> the K^-1 transform), transformed sums out (-> every
   // parameter lane); famsum is reduced straight from the transform's lanes.
   __device__ double finish_grad(V& g, double& s0) const {
+    FITOCT_MARK(finish_grad);
     const int Nn = Pr().Nn, D = Pr().D;
     const bool lik = (Pr().prior_PD == 0), poly = Pr().mode == MODE_POLY;
     const V pg = ld(V_PG), ca = ld(V_CA);   // issued up front, used last
@@ -1030,7 +1045,10 @@ struct Chain {
   // runs while the gradient waves sweep the staged position: the position-only
   // part of lp / grad, and the uniforms the coming leaf's merges will consume
   __device__ int act_prior() {
+    FITOCT_MARK(act_prior);
+    long long ts = stamp0();
     prior_part();
+    sub(7, ts);
     if (uni(Sp->state) == ST_TREE && lane == 0) {
       const int d = uni(Sp->depth), j = uni(Sp->leaf);
       const uint32_t t = (uint32_t)uni(Sp->t);
@@ -1044,11 +1062,12 @@ struct Chain {
 
   // a gradient arrived for CUR_Q: complete lp / grad, store them, dispatch
   __device__ int act_grad() {
+    FITOCT_MARK(act_grad);
     long long ts = stamp0();
     V g;
     double s0;
     const double lp = finish_grad(g, s0);
-    sub(5, ts);
+    sub(4, ts);
     st(V_CUR_G, g);
     Sp->cur_lp = lp;
     Sp->cur_s2 = s0;
@@ -1057,6 +1076,7 @@ struct Chain {
   }
 
   __device__ int act_init_state() {
+    FITOCT_MARK(act_init_state);
     V one, zero;
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
@@ -1100,6 +1120,7 @@ struct Chain {
   }
 
   __device__ int act_init_start() {
+    FITOCT_MARK(act_init_start);
     const int Nn = Pr().Nn, attempt = uni(Sp->init_attempt);
     V q;
 #pragma unroll
@@ -1124,6 +1145,7 @@ struct Chain {
   }
 
   __device__ int act_init_step() {
+    FITOCT_MARK(act_init_step);
     const V g = ld(V_CUR_G);
     double bad = 0.0;
 #pragma unroll
@@ -1148,6 +1170,7 @@ struct Chain {
   // --------------------- leapfrog (stan expl_leapfrog) -----------------------
   // A_LEAPFROG: begin_update_p + update_q from CUR with step Sp->lf_e
   __device__ int act_leapfrog() {
+    FITOCT_MARK(act_leapfrog);
     const double e = Sp->lf_e;
     V q = ld(V_CUR_Q), p = ld(V_CUR_P);
     const V g = ld(V_CUR_G), minv = ld(V_MINV);
@@ -1161,9 +1184,9 @@ struct Chain {
     return A_WRITE_MP;
   }
   __device__ int act_write_mp() {
+    FITOCT_MARK(act_write_mp);
     long long ts = stamp0();
     write_mp(ld(V_CUR_Q));
-    sub(8, ts);
     return A_YIELD;
   }
   // end_update_p with the gradient that just arrived
@@ -1178,6 +1201,7 @@ struct Chain {
 
   // ----------------- base_hmc::init_stepsize as actions ----------------------
   __device__ int act_ss_begin() {
+    FITOCT_MARK(act_ss_begin);
     const double eps = Sp->eps;
     if (eps == 0.0 || eps > 1e7 || isnan(eps)) return A_SS_FINISH;  // skipped like Stan
     Sp->ss_trial = 0;
@@ -1185,6 +1209,7 @@ struct Chain {
     return A_SS_TRIAL;
   }
   __device__ int act_ss_trial() {
+    FITOCT_MARK(act_ss_trial);
     const V minv = ld(V_MINV);
     const V p = momentum(TAG_SSMOM, (uint32_t)uni(Sp->ss_window), (uint32_t)uni(Sp->ss_trial), minv);
     Sp->ss_H0 = -Sp->smp_lp + kin(p, minv);
@@ -1195,6 +1220,7 @@ struct Chain {
     return A_LEAPFROG;
   }
   __device__ int act_ss_step() {
+    FITOCT_MARK(act_ss_step);
     const V p = finish_leapfrog(Sp->eps);
     double h = -Sp->cur_lp + kin(p, ld(V_MINV));
     if (isnan(h)) h = INFINITY;
@@ -1215,6 +1241,7 @@ struct Chain {
     return A_SS_TRIAL;
   }
   __device__ int act_ss_finish() {
+    FITOCT_MARK(act_ss_finish);
     if (uni(Sp->ss_window) == 0) return A_START_TRANSITION;
     // adapt_diag_e_nuts::transition after a metric update
     Sp->mu = log(10.0 * Sp->eps);
@@ -1226,6 +1253,7 @@ struct Chain {
 
   // ------------------------------ transition --------------------------------
   __device__ int act_start_transition() {
+    FITOCT_MARK(act_start_transition);
     Sp->state = ST_TREE;
     Sp->eps_used = Sp->eps;
     const V minv = ld(V_MINV);
@@ -1249,6 +1277,7 @@ struct Chain {
   }
 
   __device__ int act_begin_subtree() {
+    FITOCT_MARK(act_begin_subtree);
     const int d = uni(Sp->depth);
     const double u = uniform(key, (uint32_t)uni(Sp->t), TAG_DIR, (uint32_t)d, 0u);
     const int dir = (u > 0.5) ? 1 : 0;
@@ -1291,6 +1320,7 @@ struct Chain {
   // Chain scalars are read once into registers and written back once, so the
   // action costs a handful of LDS round trips instead of one per field.
   __device__ int act_leaf() {
+    FITOCT_MARK(act_leaf);
     long long ts = stamp0();
     const double e = Sp->lf_e, cur_lp = Sp->cur_lp, cur_s2 = Sp->cur_s2, H0 = Sp->H0;
     const double sum_metro0 = Sp->sum_metro;
@@ -1357,6 +1387,7 @@ struct Chain {
         return A_END_TREE;
       }
     }
+    sub(2, ts);
     if (j != (1 << d) - 1) {
       Sp->pool_used = (int)used;
       Sp->leaf = j + 1;
@@ -1414,6 +1445,7 @@ struct Chain {
     }
     const bool persist = crit3(far, p, rtot, far, Tpb, rx, near, p, ry, minv);
     st(V_RHO, rtot);
+    sub(3, ts);
     if (!persist || d + 1 >= Pr().max_depth) return A_END_TREE;
     return A_BEGIN_SUBTREE;
   }
@@ -1446,6 +1478,7 @@ struct Chain {
   }
 
   __device__ int act_end_tree() {
+    FITOCT_MARK(act_end_tree);
     const double accept = Sp->sum_metro / (double)Sp->n_leapfrog;
     const V minv = ld(V_MINV);
     const double energy = -Sp->smp_lp + kin(ld(V_SMP_P), minv);
@@ -1527,6 +1560,7 @@ struct Chain {
   }
 
   __device__ int act_next_transition() {
+    FITOCT_MARK(act_next_transition);
     Sp->t += 1;
     const int t = uni(Sp->t);
     if (t == Pr().warmup && Pr().adapt && Pr().warmup > 0) Sp->eps = exp(Sp->x_bar);  // complete_adaptation
@@ -1590,6 +1624,7 @@ struct Chain {
   }
 
   __device__ int act_finish() {
+    FITOCT_MARK(act_finish);
     Sp->state = ST_DONE;
     const V q = ld(V_SMP_Q), minv = ld(V_MINV);
 #pragma unroll
@@ -1611,6 +1646,7 @@ struct Chain {
   // run actions until the chain yields a position to the gradient waves (or finishes)
   __device__ void run(int a) {
     for (;;) {
+      FITOCT_MARK(dispatch);
       a = uni(a);
       // opaque per action: no jump threading across actions, and no address or
       // kernarg load hoisted out of the action loop (keeps register pressure local)
@@ -1845,7 +1881,12 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   } else {           // ------------------------- NUTS waves
     // the sampler is the latency-critical stage and shares each SIMD with two
     // throughput-bound gradient waves: let it win issue arbitration
-    __builtin_amdgcn_s_setprio(3);
+    switch (P.nuts_prio) {   // s_setprio takes an immediate
+      case 0: break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      default: __builtin_amdgcn_s_setprio(3); break;
+    }
     const int c = wave - NGW;
     const bool mig = P.mig != nullptr;
     if (c < (mig ? P.G : nct)) {
@@ -1860,6 +1901,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         bool in_sweep = false;   // the last run() was A_PRIOR, overlapping the chain's sweep
         // ONE call site of the action machine (it is inlined once, not per caller)
         for (;;) {
+          FITOCT_MARK(nuts_loop);
         const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
         ch.run(a);
         if (in_sweep) {

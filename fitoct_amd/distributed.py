@@ -97,3 +97,74 @@ def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=N
     return SampleOutput(draws, prob.column_names(), out.warmup_saved, meta[:, 0].copy(),
                         meta[:, 2:2 + D].copy(), meta[:, 2 + D:].copy(), total_lf,
                         out.kernel_ms, out.wall_ms, cfg.chain_offset)
+
+
+def sample_batch_sharded(probs, cfg: SamplerConfig, engine=None, device=None):
+    """FitOCT.R's batch mode over the process group (BASELINE config 5): files are
+    split into contiguous blocks over the ranks, each rank samples its block in ONE
+    batched launch (:class:`fitoct_amd.api.Batch`), and one gather brings every
+    file's draws to rank 0.  File f's chains are global chains
+    ``cfg.chain_offset + f*cfg.chains + c`` whatever the split, so the result equals
+    a single batch of all files.  Rank 0 returns one :class:`SampleOutput` per file
+    (global file order); other ranks return their local outputs.
+
+    ``engine(prob, cfg) -> SampleOutput`` samples one file on the host side (used
+    with ``gloo``); with ``nccl`` the batch writes its draws into a device tensor
+    that is gathered over RCCL.
+    """
+    import torch
+    import torch.distributed as dist
+
+    from .api import Batch
+
+    probs = list(probs)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    F, C = len(probs), cfg.chains
+    off, cnt = shard_range(F, world, rank)
+    fmax = -(-F // world)
+    if cnt == 0:
+        raise ValueError(f"rank {rank} has no files ({F} files over {world} ranks)")
+    local = replace(cfg, chain_offset=cfg.chain_offset + off * C)
+    mine = probs[off:off + cnt]
+    nccl = dist.get_backend() == "nccl"
+    if nccl:
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        local = replace(local, device=dev.index)
+        with Batch(mine, local) as b:
+            iters, ncols = b.info["iters_saved"], b.info["n_cols"]
+            buf = torch.zeros((fmax, C, iters, ncols), dtype=torch.float64, device=dev)
+            b.run(d_draws=buf.data_ptr(), stream=torch.cuda.current_stream(dev).cuda_stream)
+            outs = [b.download(p, with_draws=False) for p in range(cnt)]
+    else:
+        if engine is None:
+            from .api import sample as engine
+        outs = [engine(p, replace(local, chain_offset=local.chain_offset + i * C))
+                for i, p in enumerate(mine)]
+        iters, ncols = outs[0].draws.shape[1:]
+        buf = torch.zeros((fmax, C, iters, ncols), dtype=torch.float64)
+        for i, o in enumerate(outs):
+            buf[i] = torch.from_numpy(o.draws)
+        dev = torch.device("cpu")
+    D = outs[0].inv_metric.shape[1]
+    meta = np.zeros((fmax, C, 2 + 2 * D))
+    for i, o in enumerate(outs):
+        meta[i, :, 0] = o.stepsize
+        meta[i, 0, 1] = o.total_leapfrogs
+        meta[i, :, 2:2 + D] = o.inv_metric
+        meta[i, :, 2 + D:] = o.last_q
+    draws_all = _gather_rows(buf, world, rank)
+    meta_all = _gather_rows(torch.from_numpy(meta).to(dev), world, rank)
+    if rank != 0:
+        return outs
+    res = []
+    cols = probs[0].column_names()
+    for r in range(world):
+        o_r, n_r = shard_range(F, world, r)
+        d_r, m_r = draws_all[r].cpu().numpy(), meta_all[r].cpu().numpy()
+        for i in range(n_r):
+            m = m_r[i]
+            res.append(SampleOutput(d_r[i].copy(), cols, outs[0].warmup_saved, m[:, 0].copy(),
+                                    m[:, 2:2 + D].copy(), m[:, 2 + D:].copy(), int(m[0, 1]),
+                                    outs[0].kernel_ms, outs[0].wall_ms,
+                                    cfg.chain_offset + (o_r + i) * C))
+    return res

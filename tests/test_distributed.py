@@ -78,3 +78,45 @@ def test_gloo_world2_gather_equals_single_run(tmp_path, chains):
     np.testing.assert_array_equal(got["draws"], ref.draws)
     np.testing.assert_array_equal(got["stepsize"], ref.stepsize)
     assert int(got["lf"]) == ref.total_leapfrogs
+
+
+def _batch_problems():
+    from fitoct_amd import ExpGPProblem
+    from fitoct_amd.synth import MODULATIONS, default_prior, synth_decay
+    t0, S0 = default_prior()
+    out = []
+    for f in range(5):
+        d = synth_decay(30 + 3 * f, MODULATIONS[f % 4], 100 + f)
+        out.append(ExpGPProblem(d["x"], d["y"], d["uy"], Nn=4, gridType="extremal", theta0=t0,
+                                Sigma0=S0, prior_type="normal"))
+    return out
+
+
+def _batch_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    from fitoct_amd.api import SamplerConfig
+    from fitoct_amd.distributed import sample_batch_sharded
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        cfg = SamplerConfig(chains=2, warmup=20, samples=10, seed=5, max_treedepth=4)
+        outs = sample_batch_sharded(_batch_problems(), cfg, engine=_oracle_engine)
+        if rank == 0:
+            np.savez(os.path.join(outdir, "batch.npz"),
+                     draws=np.stack([o.draws for o in outs]),
+                     offsets=np.array([o.chain_offset for o in outs]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_batch_files_equal_single_runs(tmp_path):
+    """Config 5 over ranks: 5 files split 3 + 2; file f's chains are global chains
+    f*chains + c, so each file equals its own single run at that chain offset."""
+    from fitoct_amd.api import SamplerConfig
+    mp.spawn(_batch_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    got = np.load(tmp_path / "batch.npz")
+    np.testing.assert_array_equal(got["offsets"], [0, 2, 4, 6, 8])
+    for f, prob in enumerate(_batch_problems()):
+        ref = _oracle_engine(prob, SamplerConfig(chains=2, warmup=20, samples=10, seed=5,
+                                                 max_treedepth=4, chain_offset=2 * f))
+        np.testing.assert_array_equal(got["draws"][f], ref.draws)
