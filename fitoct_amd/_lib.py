@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfitoct.so")
+LIB_PATH = os.environ.get("FITOCT_LIB_PATH") or os.path.join(HERE, "libfitoct.so")   # override: A/B experiments
 
 PRIOR = {"normal": 0, "lasso": 1, "horseshoe": 2, "monoexp": 3}   # monoexp: FITOCT_MODEL_MONOEXP
 GRID = {"internal": 0, "extremal": 1}

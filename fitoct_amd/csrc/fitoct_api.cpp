@@ -320,9 +320,12 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   // basis mode (see kernel_params.h BasisMode)
   std::vector<double> ta, kinv, bv;
   int mode;
-  if (mono) {
+  if (mono && !pl->mixed) {
     mode = MODE_POLY;
     ta.assign(2 * (size_t)p->N, 0.0);
+  } else if (mono) {   // the mixed kernels are row-mode only: rows of zeros (dL = 0)
+    mode = MODE_ROWS;
+    B.assign((size_t)p->N * p->Nn, 0.0);
   } else if (pl->mixed) {
     mode = MODE_ROWS;
   } else {

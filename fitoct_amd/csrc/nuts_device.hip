@@ -245,6 +245,39 @@ __device__ __forceinline__ void wave_sum_n(double (&x)[N]) {
   for (int i = 0; i < N; ++i) x[i] = swap32_add(x[i], x[i]);
 }
 
+// exp on the sampler side: reduction by ln2 (hi/lo), Taylor degree 12 on
+// |r| <= ln2/2, n = round(x log2 e) from the 1.5*2^52 shifter fed straight to
+// v_ldexp_f64 (<= 2 ulp from the library exp, scripts/micro/acc.hip; no special
+// cases: x is clamped to [-746, 710], where exp is 0 / inf either way).
+__device__ __forceinline__ double fexp(double x) {
+  x = fmin(fmax(x, -746.0), 710.0);
+  const double SH = 6755399441055744.0;   // 1.5 * 2^52
+  const double t = fma(x, 1.4426950408889634, SH);
+  const double n = t - SH;
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
+  double r = fma(-n, 6.93147180369123816490e-01, x);
+  r = fma(-n, 1.90821492927058770002e-10, r);
+  double p = 2.08767569878680989792e-09;   // 1/12!
+  p = fma(p, r, 2.50521083854417187751e-08);
+  p = fma(p, r, 2.75573192239858906526e-07);
+  p = fma(p, r, 2.75573192239858906526e-06);
+  p = fma(p, r, 2.48015873015873015873e-05);
+  p = fma(p, r, 1.98412698412698412698e-04);
+  p = fma(p, r, 1.38888888888888888889e-03);
+  p = fma(p, r, 8.33333333333333333333e-03);
+  p = fma(p, r, 4.16666666666666666667e-02);
+  p = fma(p, r, 1.66666666666666666667e-01);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, ni);
+}
+// 1/x to <= 1 ulp: v_rcp_f64 and one Newton step (x finite, nonzero)
+__device__ __forceinline__ double frcp(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+
 // Multinomial trajectory weights exp(H0 - H) as extended-exponent floats
 // m * 2^e (m in [1/2, 1) or 0): the merges of base_nuts (log_sum_exp of log
 // weights, then u < exp(lsw_final - lsw_subtree)) become an add and a multiply,
@@ -260,10 +293,10 @@ __device__ __forceinline__ XF xf_norm(double m, int e) {
   return XF{f, f == 0.0 ? 0 : e + k};
 }
 __device__ __forceinline__ XF xf_exp(double x) {   // exp(x), x <= +inf; -inf -> 0
-  if (x > -700.0 && x < 700.0) return xf_norm(exp(x), 0);
+  if (x > -700.0 && x < 700.0) return xf_norm(fexp(x), 0);
   if (!(x > -INFINITY)) return XF{0.0, 0};
   const double k = floor(x * 1.4426950408889634);   // log2(e)
-  return xf_norm(exp(fma(-k, 0.6931471805599453, x)), (int)k);
+  return xf_norm(fexp(fma(-k, 0.6931471805599453, x)), (int)k);
 }
 __device__ __forceinline__ XF xf_add(XF a, XF b) {
   if (a.m == 0.0) return b;
@@ -803,16 +836,17 @@ struct Chain {
       const double a1 = qs[5 + Nn + jl], a2 = qs[5 + 2 * Nn + jl];
       const double g1 = qs[3 + Nn], g2 = qs[4 + Nn];
       u = qs[3 + jl];
-      hl = exp(fma(0.5, a2, a1) + fma(0.5, g2, g1));
+      hl = fexp(fma(0.5, a2, a1) + fma(0.5, g2, g1));
     } else {
       u = qs[3 + jl];
     }
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
-      qe[k] = (k < D && is_log(k)) ? exp(q.a[s]) : q.a[s];
+      const double ev = (k < D && is_log(k)) ? fexp(q.a[s]) : q.a[s];
+      qe[k] = ev;
+      if (s == 0 && lane < 3) MP[lane] = ev;   // theta for the gradient waves
     }
-    if (lane < 3) MP[lane] = exp(q.a[0]);
     yv = (FAM == FAM_HORSESHOE) ? u * hl : u;
     if (lane >= Nn) yv = hl = 0.0;
     if (lane < NNP) {
@@ -862,7 +896,7 @@ struct Chain {
     constexpr bool mono = FAM == FAM_MONO;   // flat theta prior, sigma = 1 (fitMonoExp)
     const double th0 = qe[0], th1 = qe[1], th2 = qe[2];
     const double usig = mono ? 0.0 : qs[D - 1], sig = mono ? 1.0 : qe[D - 1];
-    const double is2 = mono ? 1.0 : 1.0 / (sig * sig);
+    const double is2 = mono ? 1.0 : frcp(sig * sig);
     const double d0 = mono ? 0.0 : th0 - Pr().theta0[0], d1 = mono ? 0.0 : th1 - Pr().theta0[1],
                  d2 = mono ? 0.0 : th2 - Pr().theta0[2];
     const AS_CST double* Si = Pr().S0inv;
@@ -924,7 +958,7 @@ struct Chain {
           const bool r1l = k >= 5 + Nn && k < 5 + 2 * Nn, r2l = k >= 5 + 2 * Nn;
           const bool tr1 = k == 3 + Nn || r1l;
           const double cc = (k == 4 + Nn) ? 0.5 : 0.5 * Pr().nu;
-          const double e2 = ek * ek, ie = 1.0 / ek;
+          const double e2 = ek * ek, ie = frcp(ek);
           gk = tz ? -qk : tr1 ? 1.0 - e2 : cc * ie - cc;
           lpc += tz ? -0.5 * qk * qk : tr1 ? fma(-0.5, e2, qk) : -cc * (qk + ie);
           const int ai = tz ? 32 + (k - 3) : r1l ? k - 5 - Nn : r2l ? k - 5 - 2 * Nn : 0;
@@ -1049,13 +1083,15 @@ struct Chain {
     long long ts = stamp0();
     prior_part();
     sub(7, ts);
-    if (uni(Sp->state) == ST_TREE && lane == 0) {
+    if (uni(Sp->state) == ST_TREE) {   // one Philox per lane, all in parallel
       const int d = uni(Sp->depth), j = uni(Sp->leaf);
       const uint32_t t = (uint32_t)uni(Sp->t);
-      for (int l = 0; l < d && ((j >> l) & 1); ++l)
-        Sp->u_merge[l] = uniform(key, t, TAG_MERGE | ((uint32_t)l << 8) | ((uint32_t)d << 16),
-                                 (uint32_t)j, 0u);
-      if (j == (1 << d) - 1) Sp->u_top = uniform(key, t, TAG_TOP, (uint32_t)d, 0u);
+      const int nm = min(d, (int)__builtin_ctz(~(unsigned)j));   // merges: trailing ones of j
+      if (lane < nm)
+        Sp->u_merge[lane] = uniform(key, t, TAG_MERGE | ((uint32_t)lane << 8) |
+                                    ((uint32_t)d << 16), (uint32_t)j, 0u);
+      if (lane == WAVE - 1 && j == (1 << d) - 1)
+        Sp->u_top = uniform(key, t, TAG_TOP, (uint32_t)d, 0u);
     }
     return A_YIELD;
   }
