@@ -363,9 +363,14 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
         seed = int(np.random.SeedSequence().entropy & 0xFFFFFFFF)
     _, xGP = prob.basis()
     if method != "sample":
+        from .genquant import expgp_curves
         from .optim_vb import optimizing, vb
         fit = (optimizing(prob, precision=precision, device=device) if method == "optim"
                else vb(prob, seed=seed, precision=precision, device=device))
+        if method == "optim":   # fit$par$m / $resid / $dL (server.R:351,636)
+            g = expgp_curves(prob, fit.par["theta"], fit.par["yGP"])
+            for k in ("m", "resid", "dL"):
+                fit.par[k] = g[k][0]
         return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,
                 "lasso": prior_type == "lasso"}
     cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_sample, seed=seed,
