@@ -37,6 +37,9 @@ SOURCES = [
 # (read with FITOCT_STAMPS=1); production builds carry no timing code.
 PROFILE = os.environ.get("FITOCT_PROFILE", "0") not in ("", "0")
 HEADERS = ["kernel_params.h", "philox.h", "host_internal.h"]
+# FITOCT_HIPFLAGS="-DX=1 ...": extra device-compile flags for A/B variant libraries
+# (built with --force, copied aside, loaded through FITOCT_LIB_PATH)
+EXTRA = os.environ.get("FITOCT_HIPFLAGS", "").split()
 
 
 def _hipcc() -> str:
@@ -51,7 +54,7 @@ def _flags_file() -> str:
 
 
 def _flags() -> str:
-    return f"arch={ARCH} profile={int(PROFILE)}"
+    return f"arch={ARCH} profile={int(PROFILE)} extra={' '.join(EXTRA)}"
 
 
 def _newest_input() -> float:
@@ -75,6 +78,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         obj = os.path.join(OBJDIR, name + ".o")
         if PROFILE and cc == "hipcc":
             flags = flags + ["-DFITOCT_PROFILE=1"]
+        if cc == "hipcc" and EXTRA:
+            flags = flags + EXTRA
         exe = hipcc if cc == "hipcc" else (shutil.which("g++") or "g++")
         cmd = [exe, *flags, "-fPIC", "-Wall", f"-I{INCLUDE}", f"-I{CSRC}",
                "-I/opt/rocm/include", "-c", os.path.join(CSRC, src), "-o", obj]
