@@ -90,7 +90,8 @@ def cpu_baseline(prob, gpu_lf_per_step, draws_per_step):
     lf = int(o["leapfrogs"].sum())
     lf_rate = lf / wall
     value = draws_per_step * lf_rate / gpu_lf_per_step
-    return {"value": value, "unit": "draws/s", "cores": threads, "kind": "port",
+    post = o["draws"][:, W:, :] if cfg.save_warmup else o["draws"]
+    return {"means": np.nanmean(post, axis=(0, 1)), "value": value, "unit": "draws/s", "cores": threads, "kind": "port",
             "sample": (f"C oracle NUTS, {threads} chains x ({W} warmup + {S} draws) of the same "
                        f"problem on {threads} threads: {lf} gradients in {wall:.1f} s "
                        f"({lf_rate:.3g} grad/s); scaled by the GPU step's "
@@ -271,7 +272,16 @@ def main():
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(prob, float(np.mean(lf_steps)), C * S_it)
+        cb = cpu_baseline(prob, float(np.mean(lf_steps)), C * S_it)
+        o_means = cb.pop("means")
+        line["cpu_baseline"] = cb
+        # north star: posterior means within 1 % of the CPU path on the same inputs.
+        # GPU: this step's chains after warmup; oracle: the bounded CPU sample above
+        # (its own Monte-Carlo error, ~0.1 % on theta, is part of the figure).
+        g_means = np.nanmean(last[:, W_saved:, :], axis=(0, 1))
+        rel = {n: round(float(abs(g_means[j] - o_means[j]) / abs(o_means[j])), 6)
+               for j, n in enumerate(cols) if n.startswith("theta") or n in ("sigma", "br")}
+        line["posterior_mean_relerr_vs_cpu"] = rel
     for pl in plans:
         pl.close()
     if rank == 0:
