@@ -268,6 +268,10 @@ def main():
         "rhat_max": round(max(rh), 5), "stuck_chains": int(stuck.sum()),
         "rhat_max_excl_stuck": round(max(rh_free), 5), "divergent_frac": round(divergent, 5),
         "gradients_per_iteration": round(lf_per_draw, 1),
+        # sampling phase alone: the kernel is gradient-bound, so its time is
+        # apportioned by the post-warmup share of the last step's gradients (rank 0's chains)
+        "sampling_only_draws_per_s_est": round(
+            draws_step / (kms / 1e3 * float(last[:, W_saved:, 4].sum()) / outs[-1].total_leapfrogs), 1),
         "total_gradients_per_step": float(lf_all.mean()),
         "roofline": roof,
     }
