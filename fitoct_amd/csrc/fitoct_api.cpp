@@ -99,6 +99,14 @@ int check_problem(const fitoct_problem* p) {
     if (!isfinite(p->x[i]) || !isfinite(p->y[i]) || !(p->uy[i] > 0.0) || !isfinite(p->uy[i]))
       return fail(FITOCT_E_ARG, "x, y must be finite and uy > 0 at bin " + std::to_string(i));
   }
+  if (!mono && !p->B) {   // x~ = (x - min x) / (max x - min x) (server.R:635)
+    double xmin = p->x[0], xmax = p->x[0];
+    for (int i = 1; i < p->N; ++i) {
+      xmin = fmin(xmin, p->x[i]);
+      xmax = fmax(xmax, p->x[i]);
+    }
+    if (!(xmax > xmin)) return fail(FITOCT_E_ARG, "x must not be constant");
+  }
   for (int j = 0; j < 3; ++j)
     if (!(p->theta0[j] > 0.0)) return fail(FITOCT_E_ARG, "theta0 must be > 0");
   if (p->prior_type == FITOCT_PRIOR_NORMAL && !(p->lambda_rate > 0.0))

@@ -174,3 +174,29 @@ def test_missing_library_raises(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libfitoct.so"))
     with pytest.raises(ImportError):
         _lib.lib()
+
+
+@pytest.mark.parametrize("case", ["constant_x", "one_bin", "nan_y", "inf_x", "neg_uy"])
+def test_degenerate_inputs_rejected(case):
+    """Degenerate data (SURVEY.md §8 edge cases: empty / ragged / non-finite) fail with
+    FITOCT_E_ARG and a message, before any device work."""
+    from fitoct_amd.api import logp_grad
+    x = np.linspace(20, 500, 16)
+    y, uy = 1000 + 0 * x, 1 + 0 * x
+    if case == "constant_x":
+        x = 0 * x + 20.0
+    elif case == "one_bin":
+        x, y, uy = x[:1], y[:1], uy[:1]
+    elif case == "nan_y":
+        y = y.copy()
+        y[5] = np.nan
+    elif case == "inf_x":
+        x = x.copy()
+        x[0] = np.inf
+    else:
+        uy = uy.copy()
+        uy[2] = -1.0
+    prob = ExpGPProblem(x, y, uy, Nn=5)   # no Python-side value checks: the ABI must refuse
+    with pytest.raises(_lib.FitOCTError) as ei:
+        logp_grad(prob, np.zeros((1, prob.D)))
+    assert ei.value.code == -1 and len(str(ei.value)) > 0
