@@ -22,6 +22,7 @@ PREC = {"f64": 0, "mixed": 1}
 STATUS = {
     0: "FITOCT_OK", -1: "FITOCT_E_ARG", -2: "FITOCT_E_HIP", -3: "FITOCT_E_NODEVICE",
     -4: "FITOCT_E_INIT", -5: "FITOCT_E_NUMERIC", -6: "FITOCT_E_TIMEOUT", -7: "FITOCT_E_INTERNAL",
+    -8: "FITOCT_E_CANCELLED",
 }
 
 _dp = C.POINTER(C.c_double)
@@ -129,6 +130,11 @@ SIGNATURES = [
      [C.POINTER(Problem), C.POINTER(Config), C.POINTER(C.c_void_p)]),
     ("fitoct_plan_get_info", C.c_int32, [C.c_void_p, C.POINTER(PlanInfo)]),
     ("fitoct_plan_run", C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fitoct_plan_launch", C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("fitoct_plan_poll", C.c_int32, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                     C.POINTER(C.c_int32)]),
+    ("fitoct_plan_cancel", C.c_int32, [C.c_void_p]),
+    ("fitoct_plan_wait", C.c_int32, [C.c_void_p]),
     ("fitoct_plan_download", C.c_int32, [C.c_void_p, C.POINTER(Result)]),
     ("fitoct_plan_destroy", None, [C.c_void_p]),
     ("fitoct_batch_create", C.c_int32,

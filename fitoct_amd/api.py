@@ -195,11 +195,53 @@ class Plan:
         check(lib().fitoct_plan_get_info(self._h, C.byref(info)))
         self.info = {f: getattr(info, f) for f, _ in _lib.PlanInfo._fields_}
 
-    def run(self, d_draws: int = 0, stream: int = 0):
+    def run(self, d_draws: int = 0, stream: int = 0, progress=None, poll_s: float = 0.2):
         """Run on ``stream`` (hipStream_t as int); draws to the device buffer
-        ``d_draws`` (int pointer, >= info['draws_bytes']) or a plan-internal one."""
-        check(lib().fitoct_plan_run(self._h, C.c_void_p(d_draws or None),
-                                    C.c_void_p(stream or None)))
+        ``d_draws`` (int pointer, >= info['draws_bytes']) or a plan-internal one.
+
+        ``progress(done, total)``, if given, is called from this thread every
+        ``poll_s`` seconds while the kernel runs (done / total = transitions over all
+        chains; this replaces rstan's stan.log progress, server.R:457-484).  A
+        KeyboardInterrupt during the run cancels the chains at their next transition
+        boundary, waits for the kernel to drain and re-raises: the R shim does the
+        same around R_CheckUserInterrupt."""
+        if progress is None:
+            check(lib().fitoct_plan_run(self._h, C.c_void_p(d_draws or None),
+                                        C.c_void_p(stream or None)))
+            return
+        self.launch(d_draws, stream)
+        try:
+            while True:
+                done, total, finished = self.poll()
+                progress(done, total)
+                if finished:
+                    break
+                time.sleep(poll_s)
+        except KeyboardInterrupt:
+            self.cancel()
+            self.wait()
+            raise
+        self.wait()
+
+    def launch(self, d_draws: int = 0, stream: int = 0):
+        """Enqueue the run and return at once (see :meth:`poll`, :meth:`wait`)."""
+        check(lib().fitoct_plan_launch(self._h, C.c_void_p(d_draws or None),
+                                       C.c_void_p(stream or None)))
+
+    def poll(self):
+        """(transitions done over all chains, chains * (warmup + samples), finished)."""
+        d, t, f = C.c_int64(), C.c_int64(), C.c_int32()
+        check(lib().fitoct_plan_poll(self._h, C.byref(d), C.byref(t), C.byref(f)))
+        return int(d.value), int(t.value), bool(f.value)
+
+    def cancel(self):
+        """Ask every chain to stop at its next (8th) transition boundary; the run then
+        reports FITOCT_E_CANCELLED from :meth:`download`."""
+        check(lib().fitoct_plan_cancel(self._h))
+
+    def wait(self):
+        """Block until the launched run has drained."""
+        check(lib().fitoct_plan_wait(self._h))
 
     def download(self, with_draws: bool = True) -> SampleOutput:
         """Copy results to the host.  ``with_draws=False`` leaves the draws in HBM
@@ -318,14 +360,35 @@ def sample_batch(probs, cfg: SamplerConfig):
     return outs
 
 
-def sample(prob: ExpGPProblem, cfg: SamplerConfig) -> SampleOutput:
-    """One-shot sampler run (plan + run + download)."""
+def sample(prob: ExpGPProblem, cfg: SamplerConfig, progress=None) -> SampleOutput:
+    """One-shot sampler run (plan + run + download); ``progress`` as in :meth:`Plan.run`."""
     t0 = time.perf_counter()
     with Plan(prob, cfg) as pl:
-        pl.run()
+        pl.run(progress=progress)
         out = pl.download()
     out.wall_ms = (time.perf_counter() - t0) * 1e3
     return out
+
+
+def _progress_printer(chains, nb_iter, nb_warmup, stream=None):
+    """open_progress=TRUE: Stan-style progress lines ("Iteration: k / n [ p%]
+    (Warmup|Sampling)", the mean over chains) on stderr whenever 10 % more is done."""
+    import sys
+    out = stream or sys.stderr
+    last = [-1]
+
+    def cb(done, total):
+        if total <= 0:
+            return
+        pct = int(100 * done / total)
+        if pct // 10 == last[0] // 10 and pct < 100:
+            return
+        last[0] = pct
+        it = done // max(chains, 1)
+        phase = "Warmup" if it <= nb_warmup else "Sampling"
+        print(f"Iteration: {it:{len(str(nb_iter))}d} / {nb_iter} [{pct:3d}%]  ({phase}), "
+              f"{chains} chains", file=out, flush=True)
+    return cb
 
 
 # --------------------------------------------------------------------------
@@ -376,7 +439,8 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
     cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_sample, seed=seed,
                         adapt_delta=adapt_delta, max_treedepth=max_treedepth,
                         precision=precision, device=device)
-    out = sample(prob, cfg)
+    out = sample(prob, cfg, progress=_progress_printer(nb_chains, nb_iter, nb_warmup)
+                 if open_progress else None)
     fit = StanFit.from_output(out, prob)
     return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,
             "lasso": prior_type == "lasso"}

@@ -71,6 +71,10 @@ struct fitoct_plan {
   double kernel_ms = 0.0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool ran = false;
+  bool launched = false;      // fitoct_plan_launch issued, fitoct_plan_wait not yet
+  int* h_prog = nullptr;      // host-pinned [chains]: transitions done (kernel-written)
+  int* h_cancel = nullptr;    // host-pinned flag polled by the kernel
+  long long* d_stamps = nullptr;   // diagnostic stamps of the launch in flight
 };
 
 struct fitoct_evaluator {
@@ -438,6 +442,9 @@ void free_plan(fitoct_plan* pl) {
   (void)hipFree(pl->d_kp);
   (void)hipFree(pl->d_mig);
   (void)hipFree(pl->d_mig_img);
+  (void)hipFree(pl->d_stamps);
+  if (pl->h_prog) (void)hipHostFree(pl->h_prog);
+  if (pl->h_cancel) (void)hipHostFree(pl->h_cancel);
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
   if (pl->ev1) (void)hipEventDestroy(pl->ev1);
   delete pl;
@@ -697,6 +704,27 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   k.fin_q = pl->d_fin + C + (size_t)C * D;
   k.chain_status = pl->d_status;
   k.leapfrogs = pl->d_leap;
+  if (g_chains == 0) {   // progress / cancellation (fitoct_plan_poll / _cancel); batch: off
+    auto prog_setup = [&]() -> int {
+      HIP_TRY(hipHostMalloc((void**)&pl->h_prog, sizeof(int) * C,
+                            hipHostMallocMapped | hipHostMallocCoherent));
+      HIP_TRY(hipHostMalloc((void**)&pl->h_cancel, sizeof(int),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+      memset(pl->h_prog, 0, sizeof(int) * C);
+      *pl->h_cancel = 0;
+      int *dp = nullptr, *dc = nullptr;
+      HIP_TRY(hipHostGetDevicePointer((void**)&dp, pl->h_prog, 0));
+      HIP_TRY(hipHostGetDevicePointer((void**)&dc, pl->h_cancel, 0));
+      k.progress = dp;
+      k.cancel = dc;
+      return FITOCT_OK;
+    };
+    rc = prog_setup();
+    if (rc) {
+      free_plan(pl);
+      return rc;
+    }
+  }
   // Chain migration (work balance): only when every tile of the launch is
   // co-resident (one tile per CU), so an idle tile waiting for a migrant never
   // keeps a pending tile off the chip; off in batch mode (a tile holds one
@@ -742,9 +770,14 @@ int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
   return FITOCT_OK;
 }
 
-int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
+int32_t fitoct_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
   if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+  if (pl->launched) return fail(FITOCT_E_ARG, "plan is running: call fitoct_plan_wait first");
   HIP_TRY(hipSetDevice(pl->cfg.device));
+  if (pl->h_prog) {   // no launch of this plan is in flight: the kernel does not touch them
+    memset(pl->h_prog, 0, sizeof(int) * pl->kp.chains);
+    __atomic_store_n(pl->h_cancel, 0, __ATOMIC_SEQ_CST);
+  }
   double* dst = (double*)d_draws;
   if (!dst) {
     if (!pl->d_draws) HIP_TRY(hipMalloc(&pl->d_draws, pl->draws_bytes));
@@ -755,27 +788,63 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
   k.draws = dst;
   HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * k.chains, st));
   if (pl->d_mig) HIP_TRY(hipMemsetAsync(pl->d_mig, 0, pl->mig_bytes, st));
-  long long* d_stamps = nullptr;
   const bool want_stamps = getenv("FITOCT_STAMPS") != nullptr;   // diagnostic only
   if (want_stamps) {
-    HIP_TRY(hipMalloc(&d_stamps, sizeof(long long) * NSTAMP * pl->tiles));
-    HIP_TRY(hipMemsetAsync(d_stamps, 0, sizeof(long long) * NSTAMP * pl->tiles, st));
-    k.stamps = d_stamps;
+    if (!pl->d_stamps) HIP_TRY(hipMalloc(&pl->d_stamps, sizeof(long long) * NSTAMP * pl->tiles));
+    HIP_TRY(hipMemsetAsync(pl->d_stamps, 0, sizeof(long long) * NSTAMP * pl->tiles, st));
+    k.stamps = pl->d_stamps;
   }
   HIP_TRY(hipEventRecord(pl->ev0, st));
   if (!pl->d_kp) HIP_TRY(hipMalloc(&pl->d_kp, sizeof(KParams)));
   HIP_TRY(hipMemcpyAsync(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice, st));
   HIP_TRY(launch(false, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, st));
   HIP_TRY(hipEventRecord(pl->ev1, st));
+  pl->last_draws = dst;
+  pl->launched = true;
+  pl->ran = false;
+  return FITOCT_OK;
+}
+
+int32_t fitoct_plan_poll(fitoct_plan* pl, int64_t* iterations_done, int64_t* iterations_total,
+                         int32_t* finished) {
+  if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+  const int C = pl->kp.chains;
+  int64_t done = 0;
+  if (pl->h_prog)
+    for (int c = 0; c < C; ++c) done += __atomic_load_n(&pl->h_prog[c], __ATOMIC_RELAXED);
+  const int64_t total = (int64_t)C * (pl->kp.warmup + pl->kp.samples);
+  int32_t fin = pl->ran ? 1 : 0;
+  if (pl->launched) {
+    HIP_TRY(hipSetDevice(pl->cfg.device));
+    const hipError_t q = hipEventQuery(pl->ev1);
+    if (q == hipSuccess) fin = 1;
+    else if (q != hipErrorNotReady) HIP_TRY(q);
+  }
+  if (iterations_done) *iterations_done = (pl->h_prog || !fin) ? done : total;
+  if (iterations_total) *iterations_total = total;
+  if (finished) *finished = fin;
+  return FITOCT_OK;
+}
+
+int32_t fitoct_plan_cancel(fitoct_plan* pl) {
+  if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+  if (!pl->h_cancel) return fail(FITOCT_E_ARG, "this plan has no cancellation flag (batch plan)");
+  __atomic_store_n(pl->h_cancel, 1, __ATOMIC_SEQ_CST);
+  return FITOCT_OK;
+}
+
+int32_t fitoct_plan_wait(fitoct_plan* pl) {
+  if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+  if (!pl->launched) return pl->ran ? FITOCT_OK : fail(FITOCT_E_ARG, "plan has not been launched");
+  HIP_TRY(hipSetDevice(pl->cfg.device));
+  pl->launched = false;
   HIP_TRY(hipEventSynchronize(pl->ev1));
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
   pl->kernel_ms = ms;
-  pl->last_draws = dst;
-  if (want_stamps) {
+  if (pl->d_stamps && getenv("FITOCT_STAMPS") != nullptr) {
     std::vector<long long> h((size_t)NSTAMP * pl->tiles);
-    HIP_TRY(hipMemcpy(h.data(), d_stamps, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
-    (void)hipFree(d_stamps);
+    HIP_TRY(hipMemcpy(h.data(), pl->d_stamps, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
     double steps = 0, tg = 0, tn = 0, tt = 0, smax = 0, tw = 0, nw = 0, tsw = 0, tno = 0;
     double ts0 = 0, ts1 = 0;
     double act_t[18] = {0}, act_n[18] = {0};
@@ -828,6 +897,12 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
   pl->ran = true;
   return FITOCT_OK;
 }
+
+int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
+  const int32_t rc = fitoct_plan_launch(pl, d_draws, stream);
+  return rc ? rc : fitoct_plan_wait(pl);
+}
+
 
 int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
   if (!pl || !res) return fail(FITOCT_E_ARG, "NULL argument");

@@ -90,6 +90,9 @@ struct KParams {
   double* mig_img;          // [tiles * GMAX][mig_img_words] chain images in flight
   int mig_tiles, mig_img_words;
   int nuts_prio;            // s_setprio of the NUTS waves (0..3)
+  // ---- run-time progress / cancellation (host-pinned; nullptr: off) ----
+  int* progress;            // [chains] transitions completed (written at each boundary)
+  const int* cancel;        // != 0: every chain stops at its next checked boundary
   // ---- logp mode ----
   const double* q_in;       // [points][D]
   double* lp_out;           // [points]

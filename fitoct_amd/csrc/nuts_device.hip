@@ -76,7 +76,7 @@ constexpr bool kProfile = FITOCT_PROFILE != 0;
 #else
 #define FITOCT_MARK(name)
 #endif
-enum { ERR_INIT = -4, ERR_NUMERIC = -5, ERR_TIMEOUT = -6 };
+enum { ERR_INIT = -4, ERR_NUMERIC = -5, ERR_TIMEOUT = -6, ERR_CANCELLED = -8 };
 
 // vectors kept in LDS per chain (lane-private elements)
 enum VecId : int {
@@ -144,6 +144,14 @@ __device__ __forceinline__ int g_or(AS_GLB int* p, int v) {
 }
 __device__ __forceinline__ int g_and(AS_GLB int* p, int v) {
   return __hip_atomic_fetch_and((int*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// run-time progress / cancellation: host-pinned fine-grained memory, read by the
+// host while the kernel runs (system scope; at most one access per transition)
+__device__ __forceinline__ void sys_store(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ int sys_load(const int* p) {
+  return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ bool g_cas(AS_GLB int* p, int expect, int v) {
   return __hip_atomic_compare_exchange_strong((int*)p, &expect, v, __ATOMIC_RELAXED,
@@ -1599,8 +1607,15 @@ struct Chain {
     FITOCT_MARK(act_next_transition);
     Sp->t += 1;
     const int t = uni(Sp->t);
+    // transitions done, for fitoct_plan_poll (replaces rstan's stan.log progress)
+    if (Pr().progress != nullptr && lane == 0) sys_store(Pr().progress + lc, t);
     if (t == Pr().warmup && Pr().adapt && Pr().warmup > 0) Sp->eps = exp(Sp->x_bar);  // complete_adaptation
     if (t >= Pr().warmup + Pr().samples) return A_FINISH;
+    // fitoct_plan_cancel: stop at a transition boundary (checked every 8th transition)
+    if (Pr().cancel != nullptr && (t & 7) == 0 && uni(sys_load(Pr().cancel)) != 0) {
+      Sp->status = ERR_CANCELLED;
+      return A_FINISH;
+    }
     // a transition boundary: the chain's whole state is its LDS image (current
     // sample, metric, adaptation); hand it to an idle tile if this one is crowded
     if (Pr().mig != nullptr && t + 2 < Pr().warmup + Pr().samples && try_donate()) {

@@ -44,7 +44,8 @@ typedef enum fitoct_status {
   FITOCT_E_INIT = -4,      /* no finite initial point after 100 attempts */
   FITOCT_E_NUMERIC = -5,   /* step size search diverged (eps > 1e7 or eps == 0) */
   FITOCT_E_TIMEOUT = -6,   /* device step bound reached before all chains finished */
-  FITOCT_E_INTERNAL = -7
+  FITOCT_E_INTERNAL = -7,
+  FITOCT_E_CANCELLED = -8  /* fitoct_plan_cancel: chains stopped at a transition boundary */
 } fitoct_status;
 
 /* yGP hyper-prior families */
@@ -175,6 +176,23 @@ int32_t fitoct_plan_get_info(const fitoct_plan* plan, fitoct_plan_info* info);
  * non-NULL the draws go to that caller-owned DEVICE buffer (>= info.draws_bytes),
  * otherwise to a plan-internal one.  Returns after the kernel completes. */
 int32_t fitoct_plan_run(fitoct_plan* plan, void* d_draws, void* stream);
+/* The same run in two halves, for long fits driven from an interactive host.  It
+ * replaces the progress that rstan writes to stan.log and the Shiny server reads
+ * (server.R:457-484).  The R shim runs the poll loop on the R main thread, between
+ * R_CheckUserInterrupt checks (threading).
+ *   fitoct_plan_launch  enqueue the sampler on `stream` and return at once;
+ *   fitoct_plan_poll    transitions completed so far over all chains (each chain
+ *                       publishes its count at every transition boundary), the total
+ *                       chains * (warmup + samples), and whether the kernel has drained;
+ *   fitoct_plan_cancel  ask every chain to stop at its next 8th transition boundary
+ *                       (it then reports FITOCT_E_CANCELLED; the kernel drains);
+ *   fitoct_plan_wait    block until the launch has drained (then download as usual).
+ * fitoct_plan_run = launch + wait.  Batch plans have no progress/cancel channel. */
+int32_t fitoct_plan_launch(fitoct_plan* plan, void* d_draws, void* stream);
+int32_t fitoct_plan_poll(fitoct_plan* plan, int64_t* iterations_done, int64_t* iterations_total,
+                         int32_t* finished);
+int32_t fitoct_plan_cancel(fitoct_plan* plan);
+int32_t fitoct_plan_wait(fitoct_plan* plan);
 /* Copy the last run's outputs to host buffers of `res`. */
 int32_t fitoct_plan_download(fitoct_plan* plan, fitoct_result* res);
 void fitoct_plan_destroy(fitoct_plan* plan);
