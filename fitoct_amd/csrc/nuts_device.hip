@@ -718,7 +718,10 @@ struct Vd {
   double a[PPL];
 };
 
-template <int PPL, int NNP, int FAM>
+// MIG = false: a sampler built without chain migration (plans where it cannot
+// run: one chain per tile, batch mode, FITOCT_NO_MIGRATE), so the receive loop
+// and the donor check cost no registers in the NUTS waves
+template <int PPL, int NNP, int FAM, bool MIG = true>
 struct Chain {
   using V = Vd<PPL>;
   static constexpr int VLEN = WAVE * PPL;
@@ -1618,7 +1621,7 @@ struct Chain {
     }
     // a transition boundary: the chain's whole state is its LDS image (current
     // sample, metric, adaptation); hand it to an idle tile if this one is crowded
-    if (Pr().mig != nullptr && t + 2 < Pr().warmup + Pr().samples && try_donate()) {
+    if (MIG && Pr().mig != nullptr && t + 2 < Pr().warmup + Pr().samples && try_donate()) {
       Sp->state = ST_MOVED;
       return A_YIELD;
     }
@@ -1822,7 +1825,7 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane) {
 // parameter blocks, one per problem, and tile_map[2*tile] = {problem, first
 // chain} places each tile; a tile never mixes problems, so every tile still
 // keeps one problem's bins in registers.  tile_map == nullptr: one problem.
-template <class R, int BPT, int NNP, int PPL, int MODE, int FAM>
+template <class R, int BPT, int NNP, int PPL, int MODE, int FAM, bool MIG>
 __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict__ Pg,
                                                       const int* __restrict__ tile_map) {
   int pidx = 0, c0;
@@ -1856,7 +1859,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     start_max[tid] = 0;
   }
   if (tid < RINGN) ring[tid] = ~0ULL;
-  if (P.mig != nullptr) {   // every slot of the tile may host migrants: all NUTS waves live
+  if (MIG && P.mig != nullptr) {   // every slot of the tile may host migrants: all NUTS waves live
     if (tid == 0) {
       const MigView M(P.mig, P.mig_tiles);
       n_active = P.G;
@@ -1892,7 +1895,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         // hang guard: with migration a tile may idle (receivers posted) until
         // the launch's last chain ends, so the bound is in time, not polls
         if (++spins > SPIN_LIMIT) {
-          if (P.mig == nullptr) {
+          if (!MIG || P.mig == nullptr) {
             stop = true;
             break;
           }
@@ -1939,9 +1942,9 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       default: __builtin_amdgcn_s_setprio(3); break;
     }
     const int c = wave - NGW;
-    const bool mig = P.mig != nullptr;
+    const bool mig = MIG && P.mig != nullptr;
     if (c < (mig ? P.G : nct)) {
-      using Ch = Chain<PPL, NNP, FAM>;
+      using Ch = Chain<PPL, NNP, FAM, MIG>;
       long long epoch = 0;     // this slot's hand-offs (grad_cnt[c] counts NGW per epoch)
       int lc = c < nct ? c0 + c : -1;
       int a = Ch::A_INIT_STATE;
@@ -2128,7 +2131,8 @@ static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int t
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP);
   } else {
-    auto k = nuts_kernel<R, BPT, NNP, PPL, MODE, F>;
+    auto k = P.mig != nullptr ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, true>
+                              : nuts_kernel<R, BPT, NNP, PPL, MODE, F, false>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP, tile_map);
   }
