@@ -12,7 +12,8 @@ flt = sys.argv[2] if len(sys.argv) > 2 else "nuts_kernel"
 r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-DFITOCT_FAMILY={fam}",
                     "-Iinclude", "-Ifitoct_amd/csrc", "--cuda-device-only", "-c",
                     os.environ.get("SRC", "fitoct_amd/csrc/nuts_device.hip"), "-o", "/tmp/vgpr_report.o",
-                    "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
+                    "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("FITOCT_HIPFLAGS", "").split(),
+                   capture_output=True, text=True)
 cur, rows = None, {}
 for line in r.stderr.splitlines():
     m = re.search(r"Function Name: (\S+)", line)
