@@ -734,6 +734,11 @@ struct Chain {
   AS_LDS double* MP;
   AS_LDS double* part;
   const AS_LDS double* Kinv;
+  // this lane's row of K^-1 (lanes < NNP) held in VGPRs for the two K^-1 matvecs
+  // of every leaf (write_mp, finish_grad): same arithmetic, no LDS reads on the
+  // NUTS wave's critical path (configs 2 / 5 +2 %).  Not at NNP = 24 (it would spill).
+  static constexpr bool KROW = NNP <= 16;
+  double krow[KROW ? NNP : 1];
   const AS_LDS double* bv;
   int lane, slot, lc, gid, nct;
   RngKey key;
@@ -744,6 +749,15 @@ struct Chain {
         lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
     gid = Pr().chain_offset + lc;
     key = make_key(Pr().seed, (uint32_t)gid);
+    if constexpr (KROW) {
+      const int r = lane < NNP ? lane : 0;
+#pragma unroll
+      for (int k = 0; k < NNP; ++k) krow[k] = Kinv[r * NNP + k];
+    }
+  }
+  __device__ __forceinline__ double kinv_row(int k) const {
+    if constexpr (KROW) return krow[k];
+    else return Kinv[lane * NNP + k];
   }
 
   __device__ __forceinline__ KPc& Pr() const { return *pp; }
@@ -872,10 +886,10 @@ struct Chain {
         double c0 = 0.0, c1 = 0.0;   // two chains of FMAs: half the dependent latency
 #pragma unroll
         for (int k = 0; k + 1 < NNP; k += 2) {
-          c0 = fma(Kinv[lane * NNP + k], AUX[k], c0);
-          c1 = fma(Kinv[lane * NNP + k + 1], AUX[k + 1], c1);
+          c0 = fma(kinv_row(k), AUX[k], c0);
+          c1 = fma(kinv_row(k + 1), AUX[k + 1], c1);
         }
-        if constexpr ((NNP & 1) != 0) c0 = fma(Kinv[lane * NNP + NNP - 1], AUX[NNP - 1], c0);
+        if constexpr ((NNP & 1) != 0) c0 = fma(kinv_row(NNP - 1), AUX[NNP - 1], c0);
         MP[4 + lane] = (c0 + c1) * bv[lane];
       }
     }
@@ -1017,10 +1031,10 @@ struct Chain {
           double v1 = 0.0;
 #pragma unroll
           for (int m = 0; m + 1 < NNP; m += 2) {
-            v = fma(Kinv[lane * NNP + m], SUMS[4 + m], v);
-            v1 = fma(Kinv[lane * NNP + m + 1], SUMS[4 + m + 1], v1);
+            v = fma(kinv_row(m), SUMS[4 + m], v);
+            v1 = fma(kinv_row(m + 1), SUMS[4 + m + 1], v1);
           }
-          if constexpr ((NNP & 1) != 0) v = fma(Kinv[lane * NNP + NNP - 1], SUMS[4 + NNP - 1], v);
+          if constexpr ((NNP & 1) != 0) v = fma(kinv_row(NNP - 1), SUMS[4 + NNP - 1], v);
           v += v1;
           SUMS[4 + lane] = v;   // every lane's reads above precede this store
         } else {
