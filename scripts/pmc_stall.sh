@@ -1,0 +1,27 @@
+#!/bin/bash
+# Where the config-3 sampler's wave time goes: SQ wave/issue/wait cycle counters
+# (those this rocprofv3 lists), one pass, kernel-trace only.  Output gpurun_out/pmc_stall/.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/pmc_stall
+mkdir -p $OUT
+timeout -s KILL 60 rocprofv3 -L > $OUT/avail.txt 2>&1 || true
+want=""
+n=0
+for c in SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INST_CYCLES_VALU SQ_ACTIVE_INST_ANY; do
+  if grep -qw "$c" $OUT/avail.txt && [ $n -lt 8 ]; then want="$want $c"; n=$((n+1)); fi
+done
+echo "counters:$want" | tee $OUT/counters.txt
+[ -n "$want" ] || exit 0
+timeout -s KILL 120 rocprofv3 --pmc $want --output-format csv -d $OUT/p -o run -- python3 scripts/prof_small_pd.py 0 > $OUT/run.log 2>&1 || { tail -5 $OUT/run.log; exit 1; }
+python3 - "$OUT" <<'PY'
+import csv, glob, sys, collections, re
+agg = collections.defaultdict(float)
+for f in glob.glob(sys.argv[1] + "/p/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "nuts_kernel" in r.get("Kernel_Name", ""):
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+lf = int(re.search(r"leapfrogs (\d+)", open(sys.argv[1] + "/run.log").read()).group(1))
+print(f"gradients={lf}: " + ", ".join(f"{k}={v/lf:.1f}" for k, v in sorted(agg.items())) + " (per gradient)")
+PY
