@@ -1,10 +1,12 @@
 #!/bin/bash
 # Where the config-3 sampler's wave time goes: SQ wave/issue/wait cycle counters
-# (those this rocprofv3 lists), one pass, kernel-trace only.  Output gpurun_out/pmc_stall/.
+# (those this rocprofv3 lists), one pass, kernel-trace only.  Arg: prior_PD (1 = NUTS work
+# only, no sweep).  Output gpurun_out/pmc_stall<PD>/.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/pmc_stall
+PD=${1:-0}
+OUT=gpurun_out/pmc_stall$PD
 mkdir -p $OUT
 timeout -s KILL 60 rocprofv3 -L > $OUT/avail.txt 2>&1 || true
 want=""
@@ -14,7 +16,7 @@ for c in SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_IN
 done
 echo "counters:$want" | tee $OUT/counters.txt
 [ -n "$want" ] || exit 0
-timeout -s KILL 120 rocprofv3 --pmc $want --output-format csv -d $OUT/p -o run -- python3 scripts/prof_small_pd.py 0 > $OUT/run.log 2>&1 || { tail -5 $OUT/run.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc $want --output-format csv -d $OUT/p -o run -- python3 scripts/prof_small_pd.py $PD > $OUT/run.log 2>&1 || { tail -5 $OUT/run.log; exit 1; }
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections, re
 agg = collections.defaultdict(float)
