@@ -66,24 +66,66 @@ def make_problem(prior="horseshoe", N=N_BINS):
                         theta0=t0, Sigma0=S0, prior_type=prior, nu=1.0, lambda_scale=10.0)
 
 
-def make_config(seed, chains, offset, device, warmup_it, samples):
+def make_config(seed, chains, offset, device, warmup_it, samples, adapt_delta=0.8,
+                max_treedepth=10):
     from fitoct_amd import SamplerConfig
     return SamplerConfig(chains=chains, chain_offset=offset, warmup=warmup_it, samples=samples,
-                         seed=seed, adapt_delta=0.8, max_treedepth=10, device=device)
+                         seed=seed, adapt_delta=adapt_delta, max_treedepth=max_treedepth,
+                         device=device)
 
 
-def cpu_baseline(prob, gpu_lf_per_step, draws_per_step):
-    """C oracle (oracle/fitoct_oracle.c, OpenMP over chains) on ``threads`` host
-    cores: a bounded run of the same problem (one chain per thread, 250 warmup +
-    250 draws, ~10-20 s), its leapfrog rate scaled by the GPU step's leapfrogs per draw."""
-    from oracle import nuts_c
+def host_cpu_info():
+    """The host's CPUs as the bench sees them: the node's logical CPUs (``nproc``
+    of the whole machine), the CPUs this process may run on (affinity), the
+    cgroup CPU quota (``cpu.max``; a shared GPU box grants each job a share of the
+    node), and the ``lscpu`` model name."""
+    node = os.cpu_count() or 1
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
-        avail = os.cpu_count() or 1
-    threads = max(1, min(16, avail))
+        avail = node
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    sockets = set()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("physical id"):
+                    sockets.add(ln.split(":", 1)[1].strip())
+    except OSError:
+        pass
+    share = min(avail, quota) if quota else avail
+    return {"node_cpus": node, "affinity_cpus": avail, "cgroup_quota_cpus": quota,
+            "share_cpus": share, "sockets": len(sockets) or None, "model": model}
+
+
+def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, adapt_delta=0.8, max_treedepth=10):
+    """C oracle (oracle/fitoct_oracle.c, OpenMP over chains): a bounded run of the
+    same problem, one chain per host thread (250 warmup + 250 draws, ~10-20 s), its
+    leapfrog rate scaled by the GPU step's leapfrogs per draw.  It runs on every CPU
+    this job may use (affinity and cgroup quota: the job's share of a shared node);
+    chains are independent, so the node-wide rate is also given as the measured
+    per-thread rate times the node's logical CPUs (``value_node_est``)."""
+    from oracle import nuts_c
+    hw = host_cpu_info()
+    threads = hw["share_cpus"]
     W, S = 250, 250
-    cfg = make_config(7, threads, 900_000, 0, W, S)
+    cfg = make_config(7, threads, 900_000, 0, W, S, adapt_delta, max_treedepth)
     t = time.perf_counter()
     o = nuts_c.sample(prob, cfg, nthreads=threads)
     wall = time.perf_counter() - t
@@ -91,11 +133,16 @@ def cpu_baseline(prob, gpu_lf_per_step, draws_per_step):
     lf_rate = lf / wall
     value = draws_per_step * lf_rate / gpu_lf_per_step
     post = o["draws"][:, W:, :] if cfg.save_warmup else o["draws"]
-    return {"means": np.nanmean(post, axis=(0, 1)), "value": value, "unit": "draws/s", "cores": threads, "kind": "port",
+    return {"means": np.nanmean(post, axis=(0, 1)), "value": value, "unit": "draws/s",
+            "cores": threads, "kind": "port",
+            "value_node_est": value * hw["node_cpus"] / threads,
+            "host": hw,
             "sample": (f"C oracle NUTS, {threads} chains x ({W} warmup + {S} draws) of the same "
-                       f"problem on {threads} threads: {lf} gradients in {wall:.1f} s "
-                       f"({lf_rate:.3g} grad/s); scaled by the GPU step's "
-                       f"{gpu_lf_per_step / draws_per_step:.1f} gradients per post-warmup draw"),
+                       f"problem on {threads} threads (this job's CPU share of a "
+                       f"{hw['node_cpus']}-CPU node, {hw['model'] or 'unknown model'}): {lf} "
+                       f"gradients in {wall:.1f} s ({lf_rate:.3g} grad/s); scaled by the GPU "
+                       f"step's {gpu_lf_per_step / draws_per_step:.1f} gradients per "
+                       f"post-warmup draw; value_node_est = value x {hw['node_cpus']}/{threads}"),
             "wall_s": round(wall, 2)}
 
 
@@ -122,6 +169,10 @@ def main():
                     help="sampler warmup,samples per chain")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--precision", default="f64", choices=["f64", "mixed"])
+    ap.add_argument("--adapt-delta", type=float, default=0.8,
+                    help="0.8: rstan's default (the headline); 0.99 with --max-treedepth 12 is "
+                         "the reference's hard-geometry profile (Tests/testGamma.R:45)")
+    ap.add_argument("--max-treedepth", type=int, default=10)
     args = ap.parse_args()
     if args.config == 5 and args.iters == f"{WARMUP_IT},{SAMPLES}":
         args.iters = "%d,%d" % CONFIGS[5]["iters"]
@@ -156,7 +207,7 @@ def main():
 
     from fitoct_amd import Plan
     from fitoct_amd.api import SamplerConfig  # noqa: F401  (import check)
-    from fitoct_amd.stanfit import split_rhat_ess
+    from fitoct_amd.stanfit import rank_rhat, split_rhat_ess
 
     conf = CONFIGS[args.config]
     N_bins = conf["N"]
@@ -165,7 +216,8 @@ def main():
     offset = rank * C
 
     def plan_for(step):
-        cfg = make_config(1000 + step, C, offset, local, W_it, S_it)
+        cfg = make_config(1000 + step, C, offset, local, W_it, S_it, args.adapt_delta,
+                          args.max_treedepth)
         cfg.precision = args.precision
         return Plan(prob, cfg)
 
@@ -232,13 +284,16 @@ def main():
     W_saved = outs[-1].warmup_saved
     par = [j for j, n in enumerate(cols) if j >= 7 and not n.startswith("r2_")]
     rh = [split_rhat_ess(last[:, W_saved:, j])[0] for j in par]
+    rrh = [rank_rhat(last[:, W_saved:, j]) for j in par]     # Vehtari et al. 2021
     stuck = last[:, W_saved:, 5].mean(1) > 0.5       # funnel-trapped chains
     rh_free = [split_rhat_ess(last[~stuck, W_saved:, j])[0] for j in par] if stuck.any() else rh
+    rrh_free = [rank_rhat(last[~stuck, W_saved:, j]) for j in par] if stuck.any() else rrh
     divergent = float(last[:, W_saved:, 5].mean())
     lf_per_draw = float(np.mean(lf_steps)) / (C * (W_it + S_it))
 
     workload = (f"fitExpGP+{conf['prior']} N={N_bins} Nn={NN} {C} chains/GPU "
-                f"W={W_it} S={S_it} treedepth<=10")
+                f"W={W_it} S={S_it} treedepth<={args.max_treedepth}"
+                + ("" if args.adapt_delta == 0.8 else f" adapt_delta={args.adapt_delta:g}"))
     kms = float(np.mean(kernel_ms))
     flops = f_grad(N_bins, NN) * float(np.mean(lf_steps))
     achieved = flops / (kms / 1e3) / 1e12
@@ -263,10 +318,13 @@ def main():
         else "f32-sweep/f64-state", "data": "synthetic (restated synthData.R sincExp decay)",
         "config": {"workload": workload, "prior": conf["prior"], "N": N_bins, "Nn": NN,
                    "chains_per_gpu": C, "global_chains": world * C, "warmup_iters": W_it,
-                   "samples": S_it, "adapt_delta": 0.8, "max_treedepth": 10,
+                   "samples": S_it, "adapt_delta": args.adapt_delta,
+                   "max_treedepth": args.max_treedepth,
                    "parallelism": f"chains sharded over {world} GPU(s)"},
         "rhat_max": round(max(rh), 5), "stuck_chains": int(stuck.sum()),
-        "rhat_max_excl_stuck": round(max(rh_free), 5), "divergent_frac": round(divergent, 5),
+        "rhat_max_excl_stuck": round(max(rh_free), 5),
+        "rank_rhat_max": round(max(rrh), 5), "rank_rhat_max_excl_stuck": round(max(rrh_free), 5),
+        "divergent_frac": round(divergent, 5),
         "gradients_per_iteration": round(lf_per_draw, 1),
         # sampling phase alone: the kernel is gradient-bound, so its time is
         # apportioned by the post-warmup share of the last step's gradients (rank 0's chains)
@@ -276,7 +334,8 @@ def main():
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb = cpu_baseline(prob, float(np.mean(lf_steps)), C * S_it)
+        cb = cpu_baseline(prob, float(np.mean(lf_steps)), C * S_it, args.adapt_delta,
+                          args.max_treedepth)
         o_means = cb.pop("means")
         line["cpu_baseline"] = cb
         # north star: posterior means within 1 % of the CPU path on the same inputs.

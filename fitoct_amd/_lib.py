@@ -154,6 +154,19 @@ SIGNATURES = [
      [C.POINTER(Problem), C.POINTER(OptimConfig), _dp, C.POINTER(OptimResult)]),
     ("fitoct_default_vb_config", None, [C.POINTER(VbConfig)]),
     ("fitoct_vb", C.c_int32, [C.POINTER(Problem), C.POINTER(VbConfig), _dp, C.POINTER(VbResult)]),
+    ("fitoct_output_n_params", C.c_int32, [C.POINTER(Problem)]),
+    ("fitoct_output_param_name", C.c_int32, [C.POINTER(Problem), C.c_int32, C.c_char_p, C.c_int32]),
+    ("fitoct_output_rows", C.c_int32, [C.POINTER(Problem), C.c_int32, C.c_int64, _dp, _dp]),
+    ("fitoct_write_stan_csv", C.c_int32,
+     [C.c_char_p, C.POINTER(Problem), C.POINTER(Config), C.c_int32, _dp, C.c_double, _dp,
+      C.c_double, C.c_double]),
+    ("fitoct_write_vb_csv", C.c_int32,
+     [C.c_char_p, C.POINTER(Problem), C.POINTER(VbConfig), _dp, C.c_double, C.c_int32, _dp, _dp,
+      _dp, _dp, C.c_double]),
+    ("fitoct_expgp_curves", C.c_int32,
+     [C.POINTER(Problem), C.c_int32, _dp, _dp, _dp, _dp, _dp, _dp]),
+    ("fitoct_progress_line", C.c_int32,
+     [C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_char_p, C.c_int32]),
     ("fitoct_split_rhat_ess", C.c_int32, [_dp, C.c_int32, C.c_int32, _dp, _dp]),
     ("fitoct_rank_rhat", C.c_int32, [_dp, C.c_int32, C.c_int32, _dp]),
 ]

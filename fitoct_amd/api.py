@@ -10,6 +10,8 @@ with Rhat and n_eff, as used at plotExpGP.R:7-50 and server.R:88-237).
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
+import sys
 import time
 from dataclasses import dataclass, field
 
@@ -179,6 +181,7 @@ class SampleOutput:
     wall_ms: float
     chain_offset: int = 0
     migrations: int = 0        # chains handed between tiles (work balance)
+    cfg: object = None         # the SamplerConfig of the run (Stan-CSV header)
 
 
 class Plan:
@@ -262,7 +265,7 @@ class Plan:
         return SampleOutput(draws, self.prob.column_names(),
                             self.cfg.warmup if self.cfg.save_warmup else 0, eps, minv, lq,
                             int(r.total_leapfrogs), float(r.kernel_ms), 0.0,
-                            self.cfg.chain_offset, int(r.migrations))
+                            self.cfg.chain_offset, int(r.migrations), self.cfg)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -328,7 +331,9 @@ class Batch:
         return SampleOutput(draws, self.probs[problem].column_names(),
                             self.cfg.warmup if self.cfg.save_warmup else 0, eps, minv, lq,
                             int(r.total_leapfrogs), float(r.kernel_ms), 0.0,
-                            self.cfg.chain_offset + problem * C_)
+                            self.cfg.chain_offset + problem * C_, 0,
+                            dataclasses.replace(self.cfg,
+                                                chain_offset=self.cfg.chain_offset + problem * C_))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -370,24 +375,22 @@ def sample(prob: ExpGPProblem, cfg: SamplerConfig, progress=None) -> SampleOutpu
     return out
 
 
-def _progress_printer(chains, nb_iter, nb_warmup, stream=None):
-    """open_progress=TRUE: Stan-style progress lines ("Iteration: k / n [ p%]
-    (Warmup|Sampling)", the mean over chains) on stderr whenever 10 % more is done."""
-    import sys
-    out = stream or sys.stderr
+def progress_printer(warmup, samples, stream=None):
+    """rstan-format progress lines ("Chain k: Iteration: i / n [ p%]  (Warmup|Sampling)",
+    ``fitoct_progress_line``: the overall fraction in the 4-serial-chains convention the
+    Shiny server decodes, server.R:457-472) printed whenever the overall percentage
+    changes -- the lines the R shim prints to R's stdout."""
     last = [-1]
+    buf = C.create_string_buffer(160)
 
     def cb(done, total):
         if total <= 0:
             return
-        pct = int(100 * done / total)
-        if pct // 10 == last[0] // 10 and pct < 100:
+        pct = lib().fitoct_progress_line(int(done), int(total), int(warmup), int(samples), buf, 160)
+        if pct < 0 or pct == last[0]:
             return
         last[0] = pct
-        it = done // max(chains, 1)
-        phase = "Warmup" if it <= nb_warmup else "Sampling"
-        print(f"Iteration: {it:{len(str(nb_iter))}d} / {nb_iter} [{pct:3d}%]  ({phase}), "
-              f"{chains} chains", file=out, flush=True)
+        print(buf.value.decode(), file=stream or sys.stdout, flush=True)
     return cb
 
 
@@ -398,7 +401,8 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
              theta0=None, Sigma0=None, lambda_rate=0.1, rho_scale=0.0, nb_warmup=500,
              nb_iter=1000, prior_PD=0, open_progress=False, *, nb_chains=4,
              prior_type="normal", lambda_scale=10.0, nu=1.0, adapt_delta=0.8,
-             max_treedepth=10, seed=None, precision="f64", device=0, **model_switches):
+             max_treedepth=10, seed=None, precision="f64", device=0, refresh=1,
+             **model_switches):
     """Drop-in for ``FitOCTLib::fitExpGP`` (FitOCT.R:110-124).
 
     ``nb_iter`` counts warmup + sampling iterations, as the callers pass
@@ -407,6 +411,9 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
     and 'vb' run rstan::optimizing / rstan::vb natively over the same device
     density (:mod:`fitoct_amd.optim_vb`): ``fit`` is then an ``OptimFit``
     (``fit$par``, ``fit$hessian``) or a StanFit of ADVI draws.
+    Progress lines are printed to stdout in rstan's format whatever
+    ``open_progress`` is, as the R shim does (the Shiny server parses them from its
+    stdout sink, server.R:391-393,457-484); ``refresh=0`` silences them.
     Returns ``dict(fit, method, xGP, prior_PD, lasso)``.
     """
     from .stanfit import StanFit
@@ -439,8 +446,7 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
     cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_sample, seed=seed,
                         adapt_delta=adapt_delta, max_treedepth=max_treedepth,
                         precision=precision, device=device)
-    out = sample(prob, cfg, progress=_progress_printer(nb_chains, nb_iter, nb_warmup)
-                 if open_progress else None)
+    out = sample(prob, cfg, progress=progress_printer(nb_warmup, nb_sample) if refresh else None)
     fit = StanFit.from_output(out, prob)
     return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,
             "lasso": prior_type == "lasso"}

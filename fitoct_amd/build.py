@@ -32,6 +32,7 @@ SOURCES = [
     ("fitoct_api", "fitoct_api.cpp", "hipcc", [f"--offload-arch={ARCH}", "-O2", "-std=c++17"]),
     ("host_model", "host_model.cpp", "g++", ["-O2", "-std=c++17"]),
     ("optimize", "optimize.cpp", "g++", ["-O2", "-std=c++17"]),
+    ("stan_output", "stan_output.cpp", "g++", ["-O2", "-std=c++17"]),
 ]
 # FITOCT_PROFILE=1: a diagnostic build whose kernels record cycle stamps
 # (read with FITOCT_STAMPS=1); production builds carry no timing code.

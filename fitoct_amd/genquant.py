@@ -11,22 +11,34 @@ buffer by ~3N/D.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
+from . import _lib
 
-def expgp_curves(prob, theta, ygp, B=None):
-    """dict(dL, m, resid, br) for parameter rows ``theta[S, 3]``, ``ygp[S, Nn]``."""
-    theta = np.atleast_2d(np.asarray(theta, np.float64))
-    ygp = np.atleast_2d(np.asarray(ygp, np.float64))
-    if B is None:
-        B, _ = prob.basis()
-    x, y, uy = prob.x, prob.y, prob.uy
-    c = float(prob.dataType)
-    dL = ygp @ B.T
-    with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
-        m = theta[:, :1] + theta[:, 1:2] * np.exp(-c * x[None, :] / (theta[:, 2:3] * (1.0 + dL)))
-    resid = (y[None, :] - m) / uy[None, :]
-    return {"dL": dL, "m": m, "resid": resid, "br": np.mean(resid * resid, axis=1)}
+
+def expgp_curves(prob, theta, ygp=None, B=None):
+    """dict(dL, m, resid, br) for parameter rows ``theta[S, 3]``, ``ygp[S, Nn]``
+    (``ygp`` is ignored for the mono-exponential model), computed by the library
+    (``fitoct_expgp_curves``, the code the R shim uses for ``fit$par$m``)."""
+    theta = np.ascontiguousarray(np.atleast_2d(np.asarray(theta, np.float64)))
+    n, N = theta.shape[0], prob.N
+    p = prob.to_c()
+    if B is not None:
+        B = np.ascontiguousarray(B, dtype=np.float64)
+        p.B = _lib.dptr(B)
+    if prob.prior_type == "monoexp":
+        ygp = None
+    else:
+        ygp = np.ascontiguousarray(np.atleast_2d(np.asarray(ygp, np.float64)))
+        if ygp.shape != (n, prob.Nn):
+            raise ValueError(f"yGP has shape {ygp.shape}, expected {(n, prob.Nn)}")
+    dL, m, resid, br = np.empty((n, N)), np.empty((n, N)), np.empty((n, N)), np.empty(n)
+    _lib.check(_lib.lib().fitoct_expgp_curves(C.byref(p), n, _lib.dptr(theta), _lib.dptr(ygp),
+                                              _lib.dptr(dL), _lib.dptr(m), _lib.dptr(resid),
+                                              _lib.dptr(br)))
+    return {"dL": dL, "m": m, "resid": resid, "br": br}
 
 
 def generated_quantities(fit, prob, n=100, seed=None, draws=None):

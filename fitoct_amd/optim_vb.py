@@ -85,12 +85,10 @@ def param_columns(prob) -> list:
 def _named(prob, values: np.ndarray, sumr2: float) -> dict:
     """``fit$par`` (rstan as_vector=FALSE): base name -> array or scalar, with the
     transformed parameters of the horseshoe model and the Birge ratio."""
-    from .stanfit import _base, add_transformed
-    cols = param_columns(prob) + ["br"]
-    row = np.concatenate([values, [sumr2 / prob.N]])[None, :]
-    row, cols = add_transformed(row, cols, prob)
+    from .stanfit import _base, materialise, output_columns
+    row = materialise(np.concatenate([values, [sumr2 / prob.N]])[None, :], prob, n_lead=0)
     par = {}
-    for c, v in zip(cols, row[0]):
+    for c, v in zip(output_columns(prob, lead=()), row[0]):
         par.setdefault(_base(c), []).append(float(v))
     return {k: (np.array(v) if len(v) > 1 or k in ("theta", "yGP") else v[0])
             for k, v in par.items()}
@@ -151,7 +149,8 @@ def vb(prob, init=None, *, iter=10000, grad_samples=1, elbo_samples=100, eval_el
        eta=1.0, adapt_engaged=True, adapt_iter=50, tol_rel_obj=0.01, output_samples=1000,
        seed=1234, precision="f64", device=0):
     """``rstan::vb(model)`` (algorithm='meanfield', Stan defaults) -> StanFit."""
-    from .stanfit import StanFit, add_transformed
+    from .genquant import expgp_curves
+    from .stanfit import StanFit, materialise, output_columns
     c = _lib.VbConfig()
     lib().fitoct_default_vb_config(C.byref(c))
     c.iter, c.grad_samples, c.elbo_samples = int(iter), int(grad_samples), int(elbo_samples)
@@ -168,12 +167,16 @@ def vb(prob, init=None, *, iter=10000, grad_samples=1, elbo_samples=100, eval_el
     q0 = None if init is None else np.ascontiguousarray(init, dtype=np.float64).reshape(D)
     p = prob.to_c()
     check(lib().fitoct_vb(C.byref(p), C.byref(c), dptr(q0), C.byref(r)))
-    cols = ["lp__", "log_p__", "log_g__"] + param_columns(prob) + ["br"]
-    body = np.concatenate([np.zeros((S, 1)), lp[:, None], lg[:, None], constrain(prob, q),
-                           (s2 / prob.N)[:, None]], axis=1)[None]
-    body, cols = add_transformed(body, cols, prob)
+    lead = ["lp__", "log_p__", "log_g__"]
+    raw = np.concatenate([np.zeros((S, 1)), lp[:, None], lg[:, None], constrain(prob, q),
+                          (s2 / prob.N)[:, None]], axis=1)[None]
+    body, cols = materialise(raw, prob, n_lead=3), output_columns(prob, lead=lead)
     mean = _named(prob, constrain(prob, mu)[0], float("nan"))
+    # br at the mean of the approximation (the first row of CmdStan's variational CSV)
+    ygp = mean.get("yGP", np.zeros(0)) if prob.prior_type != "monoexp" else None
+    mean_s2 = float(expgp_curves(prob, mean["theta"], ygp)["br"][0] * prob.N)
     return StanFit(body, cols, 0, model_name="ExpGP (meanfield ADVI)",
+                   source=("vb", prob, c, mu, mean_s2, q, lp, lg, s2, float(r.eta)),
                    meta={"method": "vb", "mu": mu, "omega": om, "mean": mean,
                          "eta": float(r.eta), "elbo": float(r.elbo),
                          "iterations": int(r.iterations), "converged": bool(r.converged),

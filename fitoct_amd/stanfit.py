@@ -13,8 +13,10 @@ The reference's consumers use (plotExpGP.R:7-50, server.R:88-237, priPost.R:20-2
 
 Parameter naming follows Stan's flattening (``theta.1``, ``yGP.3`` ...); a
 parameter *base* name (``theta``) selects all of its elements, as in rstan.
-Transformed parameters of the horseshoe model (``yGP``, ``tau``, ``lambda``;
-Tests/horseShoePrior.stan:25-33) are derived from the draws on the host.
+The column layout (transformed parameters of the horseshoe model, ``yGP``, ``tau``,
+``lambda``, Tests/horseShoePrior.stan:25-33; the lasso's ``lambda``; ``br`` dropped
+for a prior run) and the Stan-CSV writer are the library's (include/fitoct.h,
+"Stan output"), shared with the R shim.
 R-hat / n_eff come from libfitoct's C++ diagnostics (fitoct_split_rhat_ess).
 """
 from __future__ import annotations
@@ -51,38 +53,44 @@ def rank_rhat(x: np.ndarray) -> float:
     return r.value
 
 
-def add_transformed(draws: np.ndarray, cols: list, prob):
-    """Append the transformed parameters of the horseshoe model (yGP, tau,
-    lambda; Tests/horseShoePrior.stan:25-33) before ``br`` and drop ``br`` for a
-    prior run (plotExpGP.R:42-43).  ``draws[..., len(cols)]`` in column order."""
-    cols = list(cols)
-    if prob.prior_type == "horseshoe":
-        Nn = prob.Nn
-        idx = {c: i for i, c in enumerate(cols)}
-        z = draws[..., [idx[f"z.{k+1}"] for k in range(Nn)]]
-        r1g, r2g = draws[..., idx["r1_global"]], draws[..., idx["r2_global"]]
-        r1l = draws[..., [idx[f"r1_local.{k+1}"] for k in range(Nn)]]
-        r2l = draws[..., [idx[f"r2_local.{k+1}"] for k in range(Nn)]]
-        tau = r1g * np.sqrt(r2g)
-        lam = r1l * np.sqrt(r2l)
-        ygp = z * lam * tau[..., None]
-        br_i = idx["br"]
-        extra = np.concatenate([ygp, tau[..., None], lam], axis=-1)
-        draws = np.concatenate([draws[..., :br_i], extra, draws[..., br_i:]], axis=-1)
-        cols = (cols[:br_i] + [f"yGP.{k+1}" for k in range(Nn)] + ["tau"]
-                + [f"lambda.{k+1}" for k in range(Nn)] + cols[br_i:])
-    if prob.prior_PD:   # plotExpGP.R:42-43: br is not a quantity of the prior run
-        j = cols.index("br")
-        draws = np.delete(draws, j, axis=-1)
-        cols = cols[:j] + cols[j + 1:]
-    return draws, cols
+def output_columns(prob, lead=SAMPLER_COLS) -> list:
+    """Column names of the output layout (include/fitoct.h, "Stan output"): the
+    leading columns, the model's parameters, the transformed parameters of the
+    horseshoe (``tau``, ``lambda``, ``yGP``; Tests/horseShoePrior.stan:25-33) and the
+    lasso's ``lambda``, and ``br`` unless ``prior_PD`` (plotExpGP.R:42-43)."""
+    L = _lib.lib()
+    p = prob.to_c()
+    n = L.fitoct_output_n_params(C.byref(p))
+    if n < 0:
+        _lib.check(-1)
+    buf = C.create_string_buffer(64)
+    names = []
+    for i in range(n):
+        _lib.check(L.fitoct_output_param_name(C.byref(p), i, buf, 64))
+        names.append(buf.value.decode())
+    return list(lead) + names
+
+
+def materialise(raw: np.ndarray, prob, n_lead: int = len(SAMPLER_COLS)) -> np.ndarray:
+    """Raw rows ``[..., n_lead + D + 1]`` (leading columns, constrained parameters,
+    ``br``) -> the output layout, by the library (``fitoct_output_rows``): the same
+    code that writes the Stan CSV files the R shim hands to rstan::read_stan_csv."""
+    raw = np.ascontiguousarray(raw, dtype=np.float64)
+    lead_shape = raw.shape[:-1]
+    rows = int(np.prod(lead_shape)) if lead_shape else 1
+    width = len(output_columns(prob, lead=())) + n_lead
+    out = np.empty(lead_shape + (width,))
+    p = prob.to_c()
+    _lib.check(_lib.lib().fitoct_output_rows(C.byref(p), int(n_lead), rows, _lib.dptr(raw),
+                                             _lib.dptr(out)))
+    return out
 
 
 class StanFit:
     """Draws of one sampler run: ``draws[chain, iteration, column]``."""
 
     def __init__(self, draws: np.ndarray, columns: list, warmup: int, model_name="ExpGP",
-                 stepsize=None, inv_metric=None, meta=None):
+                 stepsize=None, inv_metric=None, meta=None, source=None):
         self.columns = list(columns)
         self.warmup = int(warmup)              # leading warmup iterations stored
         self.model_name = model_name
@@ -90,16 +98,21 @@ class StanFit:
         self.inv_metric = inv_metric
         self.meta = dict(meta or {})
         self._draws = np.asarray(draws, dtype=np.float64)
+        # what the library's Stan-CSV writer needs: ("sample", prob, cfg, raw draws,
+        # kernel_ms) or ("vb", prob, vb config, mu, mean_sumr2, q, log_p, log_g, sumr2, eta)
+        self._source = source
 
     # ------------------------------------------------------------------ build
     @classmethod
-    def from_output(cls, out, prob) -> "StanFit":
-        """From a :class:`fitoct_amd.api.SampleOutput` (adds transformed parameters)."""
-        draws, cols = add_transformed(out.draws, list(out.columns), prob)
-        return cls(draws, cols, out.warmup_saved, stepsize=out.stepsize,
-                   inv_metric=out.inv_metric,
+    def from_output(cls, out, prob, cfg=None) -> "StanFit":
+        """From a :class:`fitoct_amd.api.SampleOutput`: the output layout (transformed
+        parameters added, ``br`` dropped for a prior run) by the library."""
+        cfg = cfg if cfg is not None else getattr(out, "cfg", None)
+        return cls(materialise(out.draws, prob), output_columns(prob), out.warmup_saved,
+                   stepsize=out.stepsize, inv_metric=out.inv_metric,
                    meta={"kernel_ms": out.kernel_ms, "total_leapfrogs": out.total_leapfrogs,
-                         "prior_type": prob.prior_type, "prior_PD": prob.prior_PD})
+                         "prior_type": prob.prior_type, "prior_PD": prob.prior_PD},
+                   source=("sample", prob, cfg, out.draws, out.kernel_ms))
 
     # --------------------------------------------------------------- access
     @property
@@ -174,25 +187,42 @@ class StanFit:
 
     # ------------------------------------------------------------- export
     def write_stan_csv(self, directory: str, prefix: str = "chain"):
-        """One Stan-CSV file per chain (warmup draws included, as save_warmup=1),
-        readable by ``rstan::read_stan_csv`` / CmdStan tooling."""
+        """CmdStan CSV files, one per chain (``fitoct_write_stan_csv`` /
+        ``fitoct_write_vb_csv``: the same writer the R shim uses), readable by
+        ``rstan::read_stan_csv``.  Sampled fits keep their warmup rows (save_warmup)
+        and the adaptation block; an ADVI fit gives one variational CSV."""
+        if self._source is None or (self._source[0] == "sample" and self._source[2] is None):
+            raise ValueError("this fit was not produced by the sampler or ADVI with a known "
+                             "configuration: nothing to write")
         os.makedirs(directory, exist_ok=True)
+        L = _lib.lib()
+        kind, prob = self._source[0], self._source[1]
+        p = prob.to_c()
+        if kind == "vb":
+            _, _, vcfg, mu, mean_s2, q, lp, lg, s2, eta = self._source
+            path = os.path.join(directory, f"{prefix}_vb.csv")
+            _lib.check(L.fitoct_write_vb_csv(path.encode(), C.byref(p), C.byref(vcfg),
+                                             _lib.dptr(mu), float(mean_s2), q.shape[0],
+                                             _lib.dptr(q), _lib.dptr(lp), _lib.dptr(lg),
+                                             _lib.dptr(s2), float(eta)))
+            return [path]
+        _, _, cfg, raw, kernel_ms = self._source
+        c = cfg.to_c()
+        raw = np.ascontiguousarray(raw, dtype=np.float64)
+        wrows = self.warmup
         paths = []
-        for c in range(self.chains):
-            p = os.path.join(directory, f"{prefix}_{c + 1}.csv")
-            with open(p, "w") as f:
-                f.write(f"# model = {self.model_name}\n# method = sample (Default)\n")
-                f.write(f"#   num_warmup = {self.warmup}\n#   num_samples = {self.iterations}\n")
-                f.write(f"#   save_warmup = {1 if self.warmup else 0}\n")
-                f.write(",".join(self.columns) + "\n")
-                if self.stepsize is not None:
-                    f.write("# Adaptation terminated\n")
-                    f.write(f"# Step size = {self.stepsize[c]:.8g}\n")
-                if self.inv_metric is not None:
-                    f.write("# Diagonal elements of inverse mass matrix:\n# "
-                            + ", ".join(f"{v:.8g}" for v in self.inv_metric[c]) + "\n")
-                np.savetxt(f, self._draws[c], delimiter=",", fmt="%.10g")
-            paths.append(p)
+        for ch in range(raw.shape[0]):
+            path = os.path.join(directory, f"{prefix}_{ch + 1}.csv")
+            lf = raw[ch, :, 4]           # elapsed time split by the chain's n_leapfrog__
+            t = kernel_ms / 1e3
+            tw = t * lf[:wrows].sum() / lf.sum() if lf.sum() > 0 else 0.0
+            minv = (np.ascontiguousarray(self.inv_metric[ch]) if self.inv_metric is not None
+                    else None)
+            _lib.check(L.fitoct_write_stan_csv(
+                path.encode(), C.byref(p), C.byref(c), ch, _lib.dptr(raw[ch]),
+                float(self.stepsize[ch]) if self.stepsize is not None else float("nan"),
+                _lib.dptr(minv), float(tw), float(t - tw)))
+            paths.append(path)
         return paths
 
     def __repr__(self):

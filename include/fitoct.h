@@ -317,6 +317,66 @@ void fitoct_default_vb_config(fitoct_vb_config* cfg);
 int32_t fitoct_vb(const fitoct_problem* prob, const fitoct_vb_config* cfg, const double* init_q,
                   fitoct_vb_result* res);
 
+/* ---- Stan output (host only) ------------------------------------------------ *
+ * Replaces the stanfit that rstan::sampling / rstan::vb return inside
+ * FitOCTLib::fitExpGP.  Its consumers ask for pars = c('theta','yGP','lambda','sigma',
+ * 'br','lp__') for every prior family (plotExpGP.R:9,41-43; server.R:88-237), so the
+ * output layout is the kernel's draw columns plus the model's transformed parameters,
+ * in Stan's order (parameters, transformed parameters, generated quantities):
+ *   normal    : theta[3] yGP[Nn] lambda sigma br
+ *   lasso     : theta[3] yGP[Nn] sigma lambda br        (⚑ lambda = lambda_scale, a constant:
+ *                                                        lassoPrior.stan:4 has it as data)
+ *   horseshoe : theta[3] z[Nn] r1_global r2_global r1_local[Nn] r2_local[Nn] sigma
+ *               tau lambda[Nn] yGP[Nn] br              (horseShoePrior.stan:25-33)
+ *   monoexp   : theta[3] br
+ * br is dropped when prior_PD = 1 (plotExpGP.R:42-43).  Only prior_type, Nn, prior_PD
+ * and lambda_scale of `prob` are read by the layout functions. */
+/* number and names of the output parameter columns (after any leading columns) */
+int32_t fitoct_output_n_params(const fitoct_problem* prob);
+int32_t fitoct_output_param_name(const fitoct_problem* prob, int32_t i, char* buf, int32_t buflen);
+/* raw rows [n_rows][n_lead + D + 1] (n_lead leading columns copied as they are -- 7 sampler
+ * columns for kernel draws, 0 for a bare parameter row --, then the D constrained
+ * parameters and br) -> out [n_rows][n_lead + fitoct_output_n_params] */
+int32_t fitoct_output_rows(const fitoct_problem* prob, int32_t n_lead, int64_t n_rows,
+                           const double* raw, double* out);
+/* One chain of a sampler run as a CmdStan CSV file (rstan::read_stan_csv builds the
+ * stanfit from it: print, extract, as.matrix, summary()$summary with Rhat / n_eff,
+ * traceplot(inc_warmup = TRUE), pairs).  raw: that chain's kernel draws
+ * [iters_saved][fitoct_n_cols] (warmup rows first when cfg->save_warmup); the file has
+ * the CmdStan argument header, the output columns above, the adaptation block
+ * (step size, diagonal inverse metric) between warmup and sampling rows, and the
+ * elapsed-time trailer.  `chain` indexes cfg's chains (id = chain_offset + chain + 1). */
+int32_t fitoct_write_stan_csv(const char* path, const fitoct_problem* prob,
+                              const fitoct_config* cfg, int32_t chain, const double* raw,
+                              double stepsize, const double* inv_metric /*[D] or NULL*/,
+                              double warmup_s, double sampling_s);
+/* A mean-field ADVI result as CmdStan's variational CSV (first row: the constrained mean
+ * of the approximation; then one row per unconstrained draw q[n][D] with lp__ = 0,
+ * log_p__, log_g__).  mean_sumr2 / sumr2 give br (NaN when unknown / NULL). */
+int32_t fitoct_write_vb_csv(const char* path, const fitoct_problem* prob,
+                            const fitoct_vb_config* cfg, const double* mu, double mean_sumr2,
+                            int32_t n, const double* q, const double* log_p, const double* log_g,
+                            const double* sumr2, double eta);
+/* Generated quantities of n parameter rows (plotExpGP.R:46-57 spaghetti draws,
+ * fit$par$m / fit$par$resid of plotMonoExp.R:15-16): dL = B yGP,
+ * m = theta1 + theta2 exp(-c x / (theta3 (1 + dL))), resid = (y - m) / uy, br = mean(resid^2).
+ * theta[n][3], ygp[n][Nn] (ignored for FITOCT_MODEL_MONOEXP); outputs [n][N] (br [n]),
+ * each NULL if not wanted.  The basis is prob->B or built as fitoct_build_basis does. */
+int32_t fitoct_expgp_curves(const fitoct_problem* prob, int32_t n, const double* theta,
+                            const double* ygp, double* dL, double* m, double* resid, double* br);
+
+/* rstan's progress line for a run that has completed `done` of `total` transitions
+ * (fitoct_plan_poll) with `warmup` + `samples` iterations per chain:
+ *     "Chain k: Iteration: i / n [ p%]  (Warmup|Sampling)"
+ * The Shiny server tails these lines from stan.log and decodes the overall fraction as
+ * ((k - 1) * 100 + p) / 4, i.e. it assumes 4 chains run one after another
+ * (server.R:457-472).  All chains of a fitoct run advance together, so the line encodes
+ * the run's overall fraction f = done / total in that convention: 4 f = (k - 1) + p / 100,
+ * and i = round(p / 100 * n) is the matching per-chain iteration.  Returns
+ * floor(100 f) (callers print when it changes) or a negative fitoct_status. */
+int32_t fitoct_progress_line(int64_t done, int64_t total, int32_t warmup, int32_t samples,
+                             char* buf, int32_t buflen);
+
 /* ---- diagnostics (host only) ---------------------------------------------- */
 /* x[chains][n] of one scalar: rstan legacy split-R-hat and n_eff (autocorrelation,
  * Geyer initial monotone sequence), as shown by rstan::summary (server.R:88-104). */

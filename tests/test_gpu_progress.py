@@ -98,13 +98,20 @@ def test_interrupt_in_progress_callback_cancels():
         assert ei.value.code == -8
 
 
-def test_open_progress_prints(capsys):
+def test_fitexpgp_prints_rstan_progress(capsys):
+    """open_progress = FALSE as FitOCT.R:123 and server.R:425 pass it: the rstan-format
+    lines still reach stdout, and the Shiny parser (server.R:457-472, ported in
+    tests/shiny_progress.py) reads a monotone 0..100 from them."""
+    from shiny_progress import replay
     d = synth_decay(256, "sincExp", 4)
     t0, S0 = default_prior()
     res = fitExpGP(d["x"], d["y"], d["uy"], dataType=2, Nn=8, gridType="extremal",
-                   theta0=t0, Sigma0=S0, nb_warmup=100, nb_iter=200, open_progress=True,
+                   theta0=t0, Sigma0=S0, nb_warmup=100, nb_iter=200, open_progress=False,
                    nb_chains=4, seed=3, max_treedepth=6)
-    err = capsys.readouterr().err
-    lines = [l for l in err.splitlines() if l.startswith("Iteration:")]
+    out = capsys.readouterr().out
+    lines = [l for l in out.splitlines() if l.startswith("Chain ")]
     assert lines and "[100%]" in lines[-1] and "(Sampling)" in lines[-1]
+    shown = replay(lines)
+    assert shown[-1] == 100
+    assert all(b >= a for a, b in zip(shown, shown[1:]))
     assert res["fit"] is not None

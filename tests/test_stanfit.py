@@ -22,7 +22,8 @@ def _run(family, prior_PD=0, Nn=4, chains=3):
     cfg = SamplerConfig(chains=chains, warmup=40, samples=60, seed=8, max_treedepth=6)
     o = nuts_c.sample(prob, cfg, nthreads=3)
     out = SampleOutput(o["draws"], prob.column_names(), cfg.warmup, o["stepsize"],
-                       o["inv_metric"], o["inv_metric"] * 0, int(o["leapfrogs"].sum()), 0, 0)
+                       o["inv_metric"], o["inv_metric"] * 0, int(o["leapfrogs"].sum()), 0, 0,
+                       cfg=cfg)
     return prob, cfg, StanFit.from_output(out, prob), o
 
 
@@ -77,9 +78,10 @@ def test_stan_csv_roundtrip(tmp_path):
     header = [l for l in lines if not l.startswith("#")][0].split(",")
     assert header == fit.columns
     assert any(l.startswith("# Step size") for l in lines)
+    assert any("algorithm = hmc" in l for l in lines) and any("Elapsed Time" in l for l in lines)
     rows = [l for l in lines if not l.startswith("#")][1:]
     data = np.array([[float(v) for v in r.split(",")] for r in rows])
-    np.testing.assert_allclose(data, o["draws"][1], rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(data, fit._draws[1])   # lasso: + the constant lambda column
 
 
 def test_fitexpgp_argument_contract():
