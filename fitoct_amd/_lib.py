@@ -123,6 +123,7 @@ SIGNATURES = [
     ("fitoct_n_cols", C.c_int32, [C.c_int32, C.c_int32]),
     ("fitoct_column_name", C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32]),
     ("fitoct_build_basis", C.c_int32, [C.POINTER(Problem), _dp, _dp]),
+    ("fitoct_mono_initial_theta", C.c_int32, [C.c_int32, _dp, _dp, C.c_int32, _dp]),
     ("fitoct_logp_grad", C.c_int32,
      [C.POINTER(Problem), C.c_int32, _dp, _dp, _dp, _dp, C.c_int32, C.c_int32]),
     ("fitoct_expgp_sample", C.c_int32, [C.POINTER(Problem), C.POINTER(Config), C.POINTER(Result)]),

@@ -369,4 +369,60 @@ extern "C" int32_t fitoct_constrain(int32_t prior_type, int32_t Nn, int32_t n, c
   return FITOCT_OK;
 }
 
+extern "C" int32_t fitoct_mono_initial_theta(int32_t N, const double* x, const double* y,
+                                             int32_t data_type, double* theta) {
+  using namespace fitoct;
+  try {
+    if (N < 2 || N > FITOCT_MAX_BINS || !x || !y || !theta)
+      return fail(FITOCT_E_ARG, "need x, y with 2 <= N <= FITOCT_MAX_BINS and theta_out");
+    for (int i = 0; i < N; ++i)
+      if (!isfinite(x[i]) || !isfinite(y[i])) return fail(FITOCT_E_ARG, "x and y must be finite");
+    std::vector<int> order(N);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return x[a] < x[b]; });
+    std::vector<double> xs(N), ys(N);
+    for (int i = 0; i < N; ++i) {
+      xs[i] = x[order[i]];
+      ys[i] = y[order[i]];
+    }
+    const int tail = std::min(N, std::max(3, N / 10));
+    std::vector<double> t(ys.end() - tail, ys.end());
+    std::sort(t.begin(), t.end());
+    const double t1 = (tail % 2) ? t[tail / 2] : 0.5 * (t[tail / 2 - 1] + t[tail / 2]);
+    double amax = -INFINITY;
+    for (int i = 0; i < N; ++i) amax = std::max(amax, ys[i] - t1);
+    const double thr = 0.05 * std::max(amax, 1e-12);
+    double sx = 0, sy = 0;
+    int n = 0;
+    for (int i = 0; i < N; ++i)
+      if (ys[i] - t1 > thr) {
+        sx += xs[i];
+        sy += log(ys[i] - t1);
+        ++n;
+      }
+    double slope, icpt;
+    if (n >= 3) {   // least-squares line through (x, log(y - theta1))
+      const double mx = sx / n, my = sy / n;
+      double sxy = 0, sxx = 0;
+      for (int i = 0; i < N; ++i)
+        if (ys[i] - t1 > thr) {
+          sxy += (xs[i] - mx) * (log(ys[i] - t1) - my);
+          sxx += (xs[i] - mx) * (xs[i] - mx);
+        }
+      slope = sxx > 0 ? sxy / sxx : -1.0 / std::max(xs[N - 1] - xs[0], 1e-12);
+      icpt = my - slope * mx;
+    } else {
+      slope = -1.0 / std::max(xs[N - 1] - xs[0], 1e-12);
+      icpt = log(std::max(amax, 1e-12));
+    }
+    slope = std::min(slope, -1e-12);
+    theta[0] = std::max(fabs(t1), 1e-6);
+    theta[1] = std::max(exp(icpt), 1e-6);
+    theta[2] = std::max((double)data_type / -slope, 1e-6);
+    return FITOCT_OK;
+  } catch (...) {
+    return fail(FITOCT_E_INTERNAL, "fitoct_mono_initial_theta: out of memory");
+  }
+}
+
 extern "C" const char* fitoct_last_error(void) { return fitoct::g_last_error.c_str(); }

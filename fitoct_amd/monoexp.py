@@ -18,8 +18,6 @@ log density / gradient is a launch of the HIP gradient kernel.
 """
 from __future__ import annotations
 
-import math
-
 import numpy as np
 
 from .api import ExpGPProblem, SamplerConfig, sample
@@ -28,24 +26,19 @@ from .optim_vb import OptimFit, optimizing
 
 def initial_theta(x, y, dataType=2):
     """A rough (theta1, theta2, theta3) from the data alone (log-linear fit of the
-    decay above its tail level); only the optimiser's / sampler's start."""
-    x = np.asarray(x, float)
-    y = np.asarray(y, float)
-    n = x.size
-    tail = max(3, n // 10)
-    order = np.argsort(x)
-    xs, ys = x[order], y[order]
-    t1 = float(np.median(ys[-tail:]))
-    amp = ys - t1
-    ok = amp > 0.05 * max(float(amp.max()), 1e-12)
-    if ok.sum() >= 3:
-        slope, icpt = np.polyfit(xs[ok], np.log(amp[ok]), 1)
-    else:
-        slope, icpt = -1.0 / max(xs.max() - xs.min(), 1e-12), math.log(max(amp.max(), 1e-12))
-    slope = min(slope, -1e-12)
-    t3 = float(dataType) / -slope
-    t2 = float(math.exp(icpt))
-    return np.array([max(abs(t1), 1e-6), max(t2, 1e-6), max(t3, 1e-6)])
+    decay above its tail level; ``fitoct_mono_initial_theta``, shared with the R
+    shim); only the optimiser's / sampler's start."""
+    import ctypes as C
+
+    from . import _lib
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    if x.shape != y.shape or x.ndim != 1:
+        raise ValueError("x and y must be 1-D arrays of equal length")
+    out = np.empty(3)
+    _lib.check(_lib.lib().fitoct_mono_initial_theta(x.size, _lib.dptr(x), _lib.dptr(y),
+                                                    int(dataType), _lib.dptr(out)))
+    return out
 
 
 def mono_problem(x, y, uy, dataType=2, theta0=None) -> ExpGPProblem:

@@ -35,6 +35,8 @@ extern "C" {
 #endif
 
 #define FITOCT_ABI_VERSION 1
+/* largest accepted N (depth bins): bounds every host and device allocation derived from it */
+#define FITOCT_MAX_BINS (1 << 22)
 
 typedef enum fitoct_status {
   FITOCT_OK = 0,
@@ -152,6 +154,14 @@ int32_t fitoct_dim(int32_t prior_type, int32_t Nn);
 int32_t fitoct_n_cols(int32_t prior_type, int32_t Nn);
 /* Stan-CSV style name of draw column i (lp__, accept_stat__, ..., theta.1, ...) */
 int32_t fitoct_column_name(int32_t prior_type, int32_t Nn, int32_t i, char* buf, int32_t buflen);
+
+/* FitOCTLib::fitMonoExp's starting point for theta from the data alone (x[N], y[N]):
+ * theta1 = median of the deepest max(3, N/10) bins, then a least-squares line through
+ * log(y - theta1) where y - theta1 > 5% of its maximum gives theta2 (intercept) and
+ * theta3 = dataType / -slope.  Only the optimiser's / sampler's start (⚑ FitOCTLib's
+ * own initialisation is not visible). */
+int32_t fitoct_mono_initial_theta(int32_t N, const double* x, const double* y, int32_t data_type,
+                                  double* theta_out /*[3]*/);
 
 /* ---- GP basis (host only, fp64 Cholesky) --------------------------------- */
 int32_t fitoct_build_basis(const fitoct_problem* prob, double* B_out /*[N*Nn]*/,

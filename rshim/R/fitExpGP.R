@@ -1,8 +1,11 @@
-# FitOCTLib::fitExpGP with the MI355X sampler behind it (SURVEY.md §8b).
-# Signature and return value as called at FitOCT.R:110-124, priPost.R:2-16 and
-# server.R:408-426; extra arguments are optional.  method = 'sample' runs on the GPU
-# through .Call('fitoct_R_sample') (src/fitoct_R.c); other methods, and
-# backend = 'rstan', delegate to the original FitOCTLib function.
+# FitOCTLib::fitExpGP and FitOCTLib::fitMonoExp with the MI355X engine behind them
+# (SURVEY.md §8b, §8f rows 1-3).  Signatures and return values as called at
+# FitOCT.R:95,110-124, priPost.R:2-16 and server.R:341-343,408-426; extra arguments are
+# optional.  Every method runs on the GPU through the .Call entries of src/fitoct_R.c:
+#   'sample' -> one Stan CSV per chain (fitoct_write_stan_csv) -> rstan::read_stan_csv
+#   'optim'  -> rstan::optimizing(as_vector = FALSE, hessian = TRUE)-shaped list
+#   'vb'     -> CmdStan variational CSV (fitoct_write_vb_csv) -> rstan::read_stan_csv
+# backend = 'rstan' delegates to the original FitOCTLib functions.
 
 fitoct_device_count <- function() .Call(fitoct_R_device_count)
 
@@ -16,25 +19,49 @@ fitoct_xGP <- function(Nn, gridType) {
   }
 }
 
-# one Stan CSV per chain -> rstan::read_stan_csv (a real stanfit: print, extract,
-# as.matrix, summary()$summary with Rhat / n_eff, traceplot(inc_warmup = TRUE), pairs)
-fitoct_stanfit <- function(res, nb_chains, nb_warmup, nb_iter) {
-  ncols <- length(res[[2]])
-  arr <- array(res[[1]], dim = c(ncols, nb_iter, nb_chains))   # C order: dims reversed
-  files <- vapply(seq_len(nb_chains), function(ch) {
-    f <- tempfile(fileext = '.csv')
-    writeLines(c('# model = ExpGP', '# method = sample (Default)',
-                 sprintf('#   num_samples = %d', nb_iter - nb_warmup),
-                 sprintf('#   num_warmup = %d', nb_warmup),
-                 '#   save_warmup = 1', '#   thin = 1',
-                 sprintf('# Step size = %.17g', res[[3]][ch]),
-                 paste(res[[2]], collapse = ',')), f)
-    utils::write.table(t(arr[, , ch]), f, sep = ',', append = TRUE,
-                       col.names = FALSE, row.names = FALSE)
-    f
-  }, character(1))
+fitoct_problem <- function(x, y, uy, dataType, Nn, gridType, rho_scale, theta0, Sigma0,
+                           prior, lambda_rate = 0.1, lambda_scale = 10, nu = 1, prior_PD = 0)
+  list(x = as.double(x), y = as.double(y), uy = as.double(uy),
+       dataType = as.integer(dataType), Nn = as.integer(Nn),
+       gridType = as.character(gridType), rho = as.double(rho_scale),
+       theta0 = as.double(theta0), Sigma0 = as.double(Sigma0), prior = as.integer(prior),
+       lambda_rate = as.double(lambda_rate), lambda_scale = as.double(lambda_scale),
+       nu = as.double(nu), prior_PD = as.integer(prior_PD))
+
+# sampling: stdout gets rstan-format "Chain k: Iteration: ..." lines (the Shiny server
+# parses them from its stan.log sink, server.R:391-393,457-484)
+fitoct_sample <- function(prob, nb_chains, nb_warmup, nb_iter, seed, adapt_delta,
+                          max_treedepth, device) {
+  files <- vapply(seq_len(nb_chains), function(i) tempfile(fileext = '.csv'), character(1))
   on.exit(unlink(files))
+  .Call(fitoct_R_sample, prob,
+        list(chains = as.integer(nb_chains), warmup = as.integer(nb_warmup),
+             samples = as.integer(nb_iter - nb_warmup), seed = as.double(seed),
+             adapt_delta = as.double(adapt_delta), max_treedepth = as.integer(max_treedepth),
+             device = as.integer(device)),
+        files)
   rstan::read_stan_csv(files)
+}
+
+# rstan::optimizing(as_vector = FALSE, hessian = TRUE): par grouped by base name
+# (fit$par$theta, fit$par$yGP, fit$par$lambda, fit$par$sigma, fit$par$br) plus the
+# generated m, resid, dL; hessian on the unconstrained scale with 'theta.1'-style
+# dimnames (server.R:114-126,156-172 take sqrt(-1/H[p,p]) after gsub('\\.', '', ...))
+fitoct_optimize <- function(prob, device) {
+  res <- .Call(fitoct_R_optimize, prob, list(device = as.integer(device), hessian = TRUE))
+  base <- sub('\\.[0-9]+$', '', names(res$par))
+  par <- lapply(split(unname(res$par), factor(base, levels = unique(base))), identity)
+  par$m <- res$m
+  par$resid <- res$resid
+  if (!is.null(res$dL)) par$dL <- res$dL
+  list(par = par, value = res$value, return_code = res$return_code, hessian = res$hessian)
+}
+
+fitoct_vb <- function(prob, seed, device) {
+  f <- tempfile(fileext = '.csv')
+  on.exit(unlink(f))
+  .Call(fitoct_R_vb, prob, list(seed = as.double(seed), device = as.integer(device)), f)
+  rstan::read_stan_csv(f)
 }
 
 fitExpGP <- function(x, y, uy, dataType = 2, Nn = 10, gridType = 'internal',
@@ -47,23 +74,47 @@ fitExpGP <- function(x, y, uy, dataType = 2, Nn = 10, gridType = 'internal',
                      backend = c('hip', 'rstan'), device = 0L) {
   backend <- match.arg(backend)
   prior_type <- match.arg(prior_type)
-  if (backend == 'rstan' || method != 'sample')
+  if (backend == 'rstan')
     return(FitOCTLib::fitExpGP(x = x, y = y, uy = uy, dataType = dataType, Nn = Nn,
                                gridType = gridType, method = method, theta0 = theta0,
                                Sigma0 = Sigma0, lambda_rate = lambda_rate,
                                rho_scale = rho_scale, nb_warmup = nb_warmup,
                                nb_iter = nb_iter, prior_PD = prior_PD,
                                open_progress = open_progress))
-  res <- .Call(fitoct_R_sample, as.double(x), as.double(y), as.double(uy),
-               as.integer(dataType), as.integer(Nn), as.character(gridType),
-               as.double(rho_scale), as.double(theta0), as.double(Sigma0),
-               match(prior_type, c('normal', 'lasso', 'horseshoe')) - 1L,
-               as.double(c(lambda_rate, lambda_scale, nu)), as.integer(prior_PD),
-               as.integer(nb_chains), as.integer(nb_warmup),
-               as.integer(nb_iter - nb_warmup), as.double(seed),
-               as.double(adapt_delta), as.integer(max_treedepth),
-               as.logical(open_progress), as.integer(device))
-  fit <- fitoct_stanfit(res, nb_chains, nb_warmup, nb_iter)
+  prob <- fitoct_problem(x, y, uy, dataType, Nn, gridType, rho_scale, theta0, Sigma0,
+                         match(prior_type, c('normal', 'lasso', 'horseshoe')) - 1L,
+                         lambda_rate, lambda_scale, nu, prior_PD)
+  fit <- switch(method,
+    sample = fitoct_sample(prob, nb_chains, nb_warmup, nb_iter, seed, adapt_delta,
+                           max_treedepth, device),
+    optim = fitoct_optimize(prob, device),
+    vb = fitoct_vb(prob, seed, device),
+    stop("fitExpGP: method must be 'sample', 'optim' or 'vb'"))
   list(fit = fit, method = method, xGP = fitoct_xGP(Nn, gridType), prior_PD = prior_PD,
        lasso = prior_type == 'lasso')
+}
+
+# FitOCTLib::fitMonoExp (FitOCT.R:95-97, server.R:341-343): y = theta1 + theta2
+# exp(-c x / theta3), flat prior on theta > 0 (⚑ the restated model of include/fitoct.h).
+# Returns list(fit, method, best.theta, cor.theta).
+fitMonoExp <- function(x, y, uy, dataType = 2, method = 'optim', nb_warmup = 500,
+                       nb_iter = 1500, nb_chains = 4,
+                       seed = sample.int(.Machine$integer.max, 1),
+                       backend = c('hip', 'rstan'), device = 0L) {
+  backend <- match.arg(backend)
+  if (backend == 'rstan')
+    return(FitOCTLib::fitMonoExp(x = x, y = y, uy = uy, dataType = dataType))
+  theta0 <- .Call(fitoct_R_mono_theta0, as.double(x), as.double(y), as.integer(dataType))
+  prob <- fitoct_problem(x, y, uy, dataType, 2L, 'extremal', 0, theta0, diag(3), 3L)
+  if (method == 'sample') {
+    fit <- fitoct_sample(prob, nb_chains, nb_warmup, nb_iter, seed, 0.8, 10, device)
+    th <- as.matrix(fit, pars = 'theta')
+    return(list(fit = fit, method = method, best.theta = colMeans(th), cor.theta = cor(th)))
+  }
+  if (method != 'optim') stop("fitMonoExp: method must be 'optim' or 'sample'")
+  fit <- fitoct_optimize(prob, device)
+  theta <- fit$par$theta
+  cov_q <- solve(-fit$hessian)                 # unconstrained (log theta) scale
+  cov <- cov_q * outer(theta, theta)           # delta method back to theta
+  list(fit = fit, method = method, best.theta = theta, cor.theta = cov2cor(cov))
 }

@@ -127,3 +127,40 @@ def test_gpu_sampler_matches_oracle():
     res = fitMonoExp(d["x"], d["y"], d["uy"], method="sample", nb_warmup=300, nb_iter=700,
                      nb_chains=8, seed=3)
     assert np.all(np.abs(res["best.theta"] / TRUE - 1) < 0.05)
+
+
+def _initial_theta_np(x, y, dataType=2):
+    """numpy restatement of fitoct_mono_initial_theta (include/fitoct.h)."""
+    x, y = np.asarray(x, float), np.asarray(y, float)
+    n = x.size
+    tail = max(3, n // 10)
+    order = np.argsort(x, kind="stable")
+    xs, ys = x[order], y[order]
+    t1 = float(np.median(ys[-tail:]))
+    amp = ys - t1
+    ok = amp > 0.05 * max(float(amp.max()), 1e-12)
+    if ok.sum() >= 3:
+        slope, icpt = np.polyfit(xs[ok], np.log(amp[ok]), 1)
+    else:
+        slope, icpt = -1.0 / max(xs.max() - xs.min(), 1e-12), np.log(max(amp.max(), 1e-12))
+    slope = min(slope, -1e-12)
+    return np.array([max(abs(t1), 1e-6), max(np.exp(icpt), 1e-6),
+                     max(float(dataType) / -slope, 1e-6)])
+
+
+@pytest.mark.parametrize("case", ["decay", "reversed", "flat", "two_bins", "amplitude"])
+def test_initial_theta_matches_restatement(case):
+    rng = np.random.default_rng(5)
+    x = np.linspace(20, 500, 300)
+    y = 1000 + 2000 * np.exp(-2 * x / 300) + rng.normal(0, 5, x.size)
+    dt = 2
+    if case == "reversed":
+        x, y = x[::-1].copy(), y[::-1].copy()
+    elif case == "flat":
+        y = 1000 + 0 * x
+    elif case == "two_bins":
+        x, y = x[:2].copy(), y[:2].copy()
+    elif case == "amplitude":
+        y = 20 + 80 * np.exp(-x / 150)
+        dt = 1
+    np.testing.assert_allclose(initial_theta(x, y, dt), _initial_theta_np(x, y, dt), rtol=1e-9)
