@@ -4,6 +4,7 @@ snapshot to the GPU box.
 
     python -m fitoct_amd.build [--force] [--verbose]
     FITOCT_PROFILE=1 python -m fitoct_amd.build --force   # diagnostic cycle-stamp build
+    python -m fitoct_amd.build --sanitize   # host code under ASan + UBSan -> build_san/ (CPU suite)
 """
 from __future__ import annotations
 
@@ -19,6 +20,13 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(HERE, "libfitoct.so")
 OBJDIR = os.path.join(HERE, "build")
+# --sanitize: every host translation unit under AddressSanitizer + UBSan (clang's runtime,
+# the one hipcc links), device code unchanged; for the CPU suite only
+# (scripts/cpu_sanitized_suite.sh), never shipped
+SAN_DIR = os.path.join(HERE, "build_san")
+SAN_LIB = os.path.join(SAN_DIR, "libfitoct.so")
+SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
+CLANGXX = "/opt/rocm/lib/llvm/bin/clang++"
 ARCH = os.environ.get("FITOCT_ARCH", "gfx950")
 
 _KERNEL = [f"--offload-arch={ARCH}", "-O3", "-std=c++17"]
@@ -65,23 +73,29 @@ def _newest_input() -> float:
     return max(os.path.getmtime(p) for p in paths)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile every translation unit and link ``fitoct_amd/libfitoct.so``."""
-    same_flags = os.path.exists(_flags_file()) and open(_flags_file()).read() == _flags()
-    if (not force and same_flags and os.path.exists(LIB)
-            and os.path.getmtime(LIB) >= _newest_input()):
-        return LIB
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, sanitize: bool = False) -> str:
+    """Compile every translation unit and link ``fitoct_amd/libfitoct.so`` (or, with
+    ``sanitize``, the ASan/UBSan host build ``fitoct_amd/build_san/libfitoct.so``)."""
+    objdir, lib = (SAN_DIR, SAN_LIB) if sanitize else (OBJDIR, LIB)
+    flags_file = os.path.join(objdir, "flags.txt")
+    same_flags = os.path.exists(flags_file) and open(flags_file).read() == _flags()
+    if (not force and same_flags and os.path.exists(lib)
+            and os.path.getmtime(lib) >= _newest_input()):
+        return lib
+    os.makedirs(objdir, exist_ok=True)
     hipcc = _hipcc()
 
     def compile_one(item):
         name, src, cc, flags = item
-        obj = os.path.join(OBJDIR, name + ".o")
+        obj = os.path.join(objdir, name + ".o")
         if PROFILE and cc == "hipcc":
             flags = flags + ["-DFITOCT_PROFILE=1"]
         if cc == "hipcc" and EXTRA:
             flags = flags + EXTRA
-        exe = hipcc if cc == "hipcc" else (shutil.which("g++") or "g++")
+        if sanitize:   # host side only: each -fsanitize right after -Xarch_host for hipcc
+            flags = flags + ([a for f in SAN_FLAGS for a in ("-Xarch_host", f)]
+                             if cc == "hipcc" else SAN_FLAGS + ["-g"])
+        exe = hipcc if cc == "hipcc" else (CLANGXX if sanitize else (shutil.which("g++") or "g++"))
         cmd = [exe, *flags, "-fPIC", "-Wall", f"-I{INCLUDE}", f"-I{CSRC}",
                "-I/opt/rocm/include", "-c", os.path.join(CSRC, src), "-o", obj]
         if cc != "hipcc":
@@ -95,16 +109,19 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+    if sanitize:
+        cmd += ["-fsanitize=address,undefined", "-shared-libsan"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB)
-    with open(_flags_file(), "w") as f:
+    os.replace(tmp, lib)
+    with open(flags_file, "w") as f:
         f.write(_flags())
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="--verbose" in sys.argv))
+    print(build(force="--force" in sys.argv, verbose="--verbose" in sys.argv,
+                sanitize="--sanitize" in sys.argv))

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -93,6 +94,8 @@ namespace {
 int check_problem(const fitoct_problem* p) {
   if (!p) return fail(FITOCT_E_ARG, "problem is NULL");
   if (p->N < 2) return fail(FITOCT_E_ARG, "N must be >= 2");
+  if (p->N > FITOCT_MAX_BINS)
+    return fail(FITOCT_E_ARG, "N must be <= FITOCT_MAX_BINS (" + std::to_string(FITOCT_MAX_BINS) + ")");
   if (!p->x || !p->y || !p->uy) return fail(FITOCT_E_ARG, "x, y, uy must be non-NULL");
   const bool mono = p->prior_type == FITOCT_MODEL_MONOEXP;
   if (!mono && (p->Nn < 2 || p->Nn > 24)) return fail(FITOCT_E_ARG, "Nn must be in [2, 24]");
@@ -518,98 +521,106 @@ int32_t fitoct_n_cols(int32_t prior_type, int32_t Nn) {
 }
 
 int32_t fitoct_column_name(int32_t prior_type, int32_t Nn, int32_t i, char* buf, int32_t buflen) {
-  const std::string s = column_name(prior_type, Nn, i);
-  if (s.empty()) return fail(FITOCT_E_ARG, "column index out of range");
-  if (!buf || buflen < (int32_t)s.size() + 1) return fail(FITOCT_E_ARG, "buffer too small");
-  memcpy(buf, s.c_str(), s.size() + 1);
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    const std::string s = column_name(prior_type, Nn, i);
+    if (s.empty()) return fail(FITOCT_E_ARG, "column index out of range");
+    if (!buf || buflen < (int32_t)s.size() + 1) return fail(FITOCT_E_ARG, "buffer too small");
+    memcpy(buf, s.c_str(), s.size() + 1);
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_build_basis(const fitoct_problem* prob, double* B_out, double* xGP_out) {
-  if (!prob || !B_out) return fail(FITOCT_E_ARG, "NULL argument");
-  if (prob->N < 2 || !prob->x) return fail(FITOCT_E_ARG, "need x with N >= 2");
-  std::vector<double> B, xg;
-  const int rc = build_basis(prob, B, xg);
-  if (rc) return rc;
-  memcpy(B_out, B.data(), B.size() * sizeof(double));
-  if (xGP_out) memcpy(xGP_out, xg.data(), xg.size() * sizeof(double));
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    if (!prob || !B_out) return fail(FITOCT_E_ARG, "NULL argument");
+    if (prob->N < 2 || !prob->x) return fail(FITOCT_E_ARG, "need x with N >= 2");
+    std::vector<double> B, xg;
+    const int rc = build_basis(prob, B, xg);
+    if (rc) return rc;
+    memcpy(B_out, B.data(), B.size() * sizeof(double));
+    if (xGP_out) memcpy(xGP_out, xg.data(), xg.size() * sizeof(double));
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_evaluator_create(const fitoct_problem* prob, int32_t capacity, int32_t precision,
                                 int32_t device, fitoct_evaluator** out) {
-  if (!out) return fail(FITOCT_E_ARG, "out is NULL");
-  *out = nullptr;
-  if (capacity < 1) return fail(FITOCT_E_ARG, "capacity must be >= 1");
-  fitoct_evaluator* ev = new fitoct_evaluator();
-  ev->pl = new fitoct_plan();
-  int rc = plan_common(ev->pl, prob, capacity, precision, device, 0);
-  ev->pl->cfg.device = device;
-  auto run = [&]() -> int {
+  return guarded(__func__, [&]() -> int32_t {
+    if (!out) return fail(FITOCT_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (capacity < 1) return fail(FITOCT_E_ARG, "capacity must be >= 1");
+    // released on every early return or exception until handed to the caller
+    std::unique_ptr<fitoct_evaluator, void (*)(fitoct_evaluator*)> guard(new fitoct_evaluator(),
+                                                                       fitoct_evaluator_destroy);
+    fitoct_evaluator* ev = guard.get();
+    ev->pl = new fitoct_plan();
+    int rc = plan_common(ev->pl, prob, capacity, precision, device, 0);
+    ev->pl->cfg.device = device;
+    auto run = [&]() -> int {
+      if (rc) return rc;
+      const int D = ev->pl->kp.D;
+      ev->capacity = capacity;
+      ev->D = D;
+      ev->lp_const = lp_constant(prob);
+      ev->logmask.resize(D);
+      for (int j = 0; j < D; ++j) ev->logmask[j] = log_transformed(prob->prior_type, prob->Nn, j);
+      HIP_TRY(hipMalloc(&ev->d_q, sizeof(double) * (size_t)capacity * D));
+      HIP_TRY(hipMalloc(&ev->d_out, sizeof(double) * (size_t)capacity * (D + 2)));
+      HIP_TRY(hipMalloc(&ev->pl->d_kp, sizeof(KParams)));
+      KParams& k = ev->pl->kp;
+      k.q_in = ev->d_q;
+      k.grad_out = ev->d_out;
+      return FITOCT_OK;
+    };
+    rc = run();
     if (rc) return rc;
-    const int D = ev->pl->kp.D;
-    ev->capacity = capacity;
-    ev->D = D;
-    ev->lp_const = lp_constant(prob);
-    ev->logmask.resize(D);
-    for (int j = 0; j < D; ++j) ev->logmask[j] = log_transformed(prob->prior_type, prob->Nn, j);
-    HIP_TRY(hipMalloc(&ev->d_q, sizeof(double) * (size_t)capacity * D));
-    HIP_TRY(hipMalloc(&ev->d_out, sizeof(double) * (size_t)capacity * (D + 2)));
-    HIP_TRY(hipMalloc(&ev->pl->d_kp, sizeof(KParams)));
-    KParams& k = ev->pl->kp;
-    k.q_in = ev->d_q;
-    k.grad_out = ev->d_out;
+    *out = guard.release();
     return FITOCT_OK;
-  };
-  rc = run();
-  if (rc) {
-    fitoct_evaluator_destroy(ev);
-    return rc;
-  }
-  *out = ev;
-  return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_evaluator_run(fitoct_evaluator* ev, int32_t n, const double* q, int32_t jacobian,
                              int32_t normalised, double* lp_out, double* grad_out,
                              double* sumr2_out) {
-  if (!ev || !q || !lp_out) return fail(FITOCT_E_ARG, "bad buffers");
-  if (n < 1 || n > ev->capacity) return fail(FITOCT_E_ARG, "n_points must be in [1, capacity]");
-  fitoct_plan* pl = ev->pl;
-  KParams& k = pl->kp;
-  const int D = ev->D;
-  HIP_TRY(hipSetDevice(pl->cfg.device));
-  if (n != ev->cur_n) {  // outputs are laid out for n points: grad[n][D] | lp[n] | sumr2[n]
-    k.chains = n;
-    k.lp_out = ev->d_out + (size_t)n * D;
-    k.s2_out = k.lp_out + n;
-    pl->tiles = (n + k.G - 1) / k.G;
-    HIP_TRY(hipMemcpy(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
-    ev->cur_n = n;
-  }
-  HIP_TRY(hipMemcpy(ev->d_q, q, sizeof(double) * (size_t)n * D, hipMemcpyHostToDevice));
-  HIP_TRY(launch(true, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, 0));
-  // one copy back of grad | lp | sumr2 (contiguous)
-  ev->host.resize((size_t)n * (D + 2));
-  HIP_TRY(hipMemcpy(ev->host.data(), ev->d_out, sizeof(double) * ev->host.size(),
-                    hipMemcpyDeviceToHost));
-  const double* g = ev->host.data();
-  const double* lp = g + (size_t)n * D;
-  for (int i = 0; i < n; ++i) {
-    double v = lp[i];
-    const double* qi = q + (size_t)i * D;
-    if (!jacobian)
-      for (int j = 0; j < D; ++j)
-        if (ev->logmask[j]) v -= qi[j];
-    if (normalised) v += ev->lp_const;
-    lp_out[i] = isfinite(lp[i]) ? v : -INFINITY;
-    if (grad_out)
-      for (int j = 0; j < D; ++j)
-        grad_out[(size_t)i * D + j] = g[(size_t)i * D + j] - ((!jacobian && ev->logmask[j]) ? 1.0 : 0.0);
-    if (sumr2_out) sumr2_out[i] = lp[n + i];
-  }
-  ev->evals += n;
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    if (!ev || !q || !lp_out) return fail(FITOCT_E_ARG, "bad buffers");
+    if (n < 1 || n > ev->capacity) return fail(FITOCT_E_ARG, "n_points must be in [1, capacity]");
+    fitoct_plan* pl = ev->pl;
+    KParams& k = pl->kp;
+    const int D = ev->D;
+    HIP_TRY(hipSetDevice(pl->cfg.device));
+    if (n != ev->cur_n) {  // outputs are laid out for n points: grad[n][D] | lp[n] | sumr2[n]
+      k.chains = n;
+      k.lp_out = ev->d_out + (size_t)n * D;
+      k.s2_out = k.lp_out + n;
+      pl->tiles = (n + k.G - 1) / k.G;
+      HIP_TRY(hipMemcpy(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice));
+      ev->cur_n = n;
+    }
+    HIP_TRY(hipMemcpy(ev->d_q, q, sizeof(double) * (size_t)n * D, hipMemcpyHostToDevice));
+    HIP_TRY(launch(true, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, 0));
+    // one copy back of grad | lp | sumr2 (contiguous)
+    ev->host.resize((size_t)n * (D + 2));
+    HIP_TRY(hipMemcpy(ev->host.data(), ev->d_out, sizeof(double) * ev->host.size(),
+                      hipMemcpyDeviceToHost));
+    const double* g = ev->host.data();
+    const double* lp = g + (size_t)n * D;
+    for (int i = 0; i < n; ++i) {
+      double v = lp[i];
+      const double* qi = q + (size_t)i * D;
+      if (!jacobian)
+        for (int j = 0; j < D; ++j)
+          if (ev->logmask[j]) v -= qi[j];
+      if (normalised) v += ev->lp_const;
+      lp_out[i] = isfinite(lp[i]) ? v : -INFINITY;
+      if (grad_out)
+        for (int j = 0; j < D; ++j)
+          grad_out[(size_t)i * D + j] = g[(size_t)i * D + j] - ((!jacobian && ev->logmask[j]) ? 1.0 : 0.0);
+      if (sumr2_out) sumr2_out[i] = lp[n + i];
+    }
+    ev->evals += n;
+    return FITOCT_OK;
+  });
 }
 
 void fitoct_evaluator_destroy(fitoct_evaluator* ev) {
@@ -623,18 +634,22 @@ void fitoct_evaluator_destroy(fitoct_evaluator* ev) {
 int32_t fitoct_logp_grad(const fitoct_problem* prob, int32_t n_points, const double* q,
                          double* lp_out, double* grad_out, double* sumr2_out, int32_t precision,
                          int32_t device) {
-  if (n_points < 1 || !q || !lp_out || !grad_out) return fail(FITOCT_E_ARG, "bad buffers");
-  fitoct_evaluator* ev = nullptr;
-  int rc = fitoct_evaluator_create(prob, n_points, precision, device, &ev);
-  if (rc) return rc;
-  rc = fitoct_evaluator_run(ev, n_points, q, 1, 0, lp_out, grad_out, sumr2_out);
-  fitoct_evaluator_destroy(ev);
-  return rc;
+  return guarded(__func__, [&]() -> int32_t {
+    if (n_points < 1 || !q || !lp_out || !grad_out) return fail(FITOCT_E_ARG, "bad buffers");
+    fitoct_evaluator* ev = nullptr;
+    int rc = fitoct_evaluator_create(prob, n_points, precision, device, &ev);
+    if (rc) return rc;
+    rc = fitoct_evaluator_run(ev, n_points, q, 1, 0, lp_out, grad_out, sumr2_out);
+    fitoct_evaluator_destroy(ev);
+    return rc;
+  });
 }
 
 int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
                            fitoct_plan** out) {
-  return plan_create(prob, cfg, 0, -1, out);
+  return guarded(__func__, [&]() -> int32_t {
+    return plan_create(prob, cfg, 0, -1, out);
+  });
 }
 
 }  // extern "C"
@@ -652,13 +667,12 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   if (!(cfg->adapt_delta > 0.0 && cfg->adapt_delta < 1.0))
     return fail(FITOCT_E_ARG, "adapt_delta must be in (0, 1)");
   if (!(cfg->stepsize > 0.0)) return fail(FITOCT_E_ARG, "stepsize must be > 0");
-  fitoct_plan* pl = new fitoct_plan();
+  // released on every early return or exception until handed to the caller
+  std::unique_ptr<fitoct_plan, void (*)(fitoct_plan*)> guard(new fitoct_plan(), free_plan);
+  fitoct_plan* pl = guard.get();
   int rc = plan_common(pl, prob, cfg->chains, cfg->precision, cfg->device, cfg->max_treedepth,
                        g_chains, force_bpt);
-  if (rc) {
-    free_plan(pl);
-    return rc;
-  }
+  if (rc) return rc;
   pl->cfg = *cfg;
   KParams& k = pl->kp;
   const int C = cfg->chains, D = k.D;
@@ -694,10 +708,7 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
     return FITOCT_OK;
   };
   rc = setup();
-  if (rc) {
-    free_plan(pl);
-    return rc;
-  }
+  if (rc) return rc;
   k.stack = pl->d_stack;
   k.fin_eps = pl->d_fin;
   k.fin_minv = pl->d_fin + C;
@@ -720,10 +731,7 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
       return FITOCT_OK;
     };
     rc = prog_setup();
-    if (rc) {
-      free_plan(pl);
-      return rc;
-    }
+    if (rc) return rc;
   }
   // Chain migration (work balance): only when every tile of the launch is
   // co-resident (one tile per CU), so an idle tile waiting for a migrant never
@@ -738,16 +746,13 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
       return FITOCT_OK;
     };
     rc = mig_setup();
-    if (rc) {
-      free_plan(pl);
-      return rc;
-    }
+    if (rc) return rc;
     k.mig = pl->d_mig;
     k.mig_img = pl->d_mig_img;
     k.mig_tiles = T;
     k.mig_img_words = words;
   }
-  *out = pl;
+  *out = guard.release();
   return FITOCT_OK;
 }
 }  // namespace
@@ -755,219 +760,239 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
 extern "C" {
 
 int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
-  if (!pl || !info) return fail(FITOCT_E_ARG, "NULL argument");
-  info->dim = pl->kp.D;
-  info->n_cols = pl->kp.ncols;
-  info->iters_saved = pl->kp.iters_saved;
-  info->chains = pl->kp.chains;
-  info->tiles = pl->tiles;
-  info->chains_per_tile = pl->kp.G;
-  info->bins_per_thread = pl->bpt;
-  info->threads_per_tile = TPB;
-  info->lds_bytes = pl->lds;
-  info->n_pad = pl->kp.n_pad;
-  info->draws_bytes = (int64_t)pl->draws_bytes;
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    if (!pl || !info) return fail(FITOCT_E_ARG, "NULL argument");
+    info->dim = pl->kp.D;
+    info->n_cols = pl->kp.ncols;
+    info->iters_saved = pl->kp.iters_saved;
+    info->chains = pl->kp.chains;
+    info->tiles = pl->tiles;
+    info->chains_per_tile = pl->kp.G;
+    info->bins_per_thread = pl->bpt;
+    info->threads_per_tile = TPB;
+    info->lds_bytes = pl->lds;
+    info->n_pad = pl->kp.n_pad;
+    info->draws_bytes = (int64_t)pl->draws_bytes;
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
-  if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
-  if (pl->launched) return fail(FITOCT_E_ARG, "plan is running: call fitoct_plan_wait first");
-  HIP_TRY(hipSetDevice(pl->cfg.device));
-  if (pl->h_prog) {   // no launch of this plan is in flight: the kernel does not touch them
-    memset(pl->h_prog, 0, sizeof(int) * pl->kp.chains);
-    __atomic_store_n(pl->h_cancel, 0, __ATOMIC_SEQ_CST);
-  }
-  double* dst = (double*)d_draws;
-  if (!dst) {
-    if (!pl->d_draws) HIP_TRY(hipMalloc(&pl->d_draws, pl->draws_bytes));
-    dst = pl->d_draws;
-  }
-  hipStream_t st = (hipStream_t)stream;
-  KParams k = pl->kp;
-  k.draws = dst;
-  HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * k.chains, st));
-  if (pl->d_mig) HIP_TRY(hipMemsetAsync(pl->d_mig, 0, pl->mig_bytes, st));
-  const bool want_stamps = getenv("FITOCT_STAMPS") != nullptr;   // diagnostic only
-  if (want_stamps) {
-    if (!pl->d_stamps) HIP_TRY(hipMalloc(&pl->d_stamps, sizeof(long long) * NSTAMP * pl->tiles));
-    HIP_TRY(hipMemsetAsync(pl->d_stamps, 0, sizeof(long long) * NSTAMP * pl->tiles, st));
-    k.stamps = pl->d_stamps;
-  }
-  HIP_TRY(hipEventRecord(pl->ev0, st));
-  if (!pl->d_kp) HIP_TRY(hipMalloc(&pl->d_kp, sizeof(KParams)));
-  HIP_TRY(hipMemcpyAsync(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice, st));
-  HIP_TRY(launch(false, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, st));
-  HIP_TRY(hipEventRecord(pl->ev1, st));
-  pl->last_draws = dst;
-  pl->launched = true;
-  pl->ran = false;
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    if (pl->launched) return fail(FITOCT_E_ARG, "plan is running: call fitoct_plan_wait first");
+    HIP_TRY(hipSetDevice(pl->cfg.device));
+    if (pl->h_prog) {   // no launch of this plan is in flight: the kernel does not touch them
+      memset(pl->h_prog, 0, sizeof(int) * pl->kp.chains);
+      __atomic_store_n(pl->h_cancel, 0, __ATOMIC_SEQ_CST);
+    }
+    double* dst = (double*)d_draws;
+    if (!dst) {
+      if (!pl->d_draws) HIP_TRY(hipMalloc(&pl->d_draws, pl->draws_bytes));
+      dst = pl->d_draws;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    KParams k = pl->kp;
+    k.draws = dst;
+    HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * k.chains, st));
+    if (pl->d_mig) HIP_TRY(hipMemsetAsync(pl->d_mig, 0, pl->mig_bytes, st));
+    const bool want_stamps = getenv("FITOCT_STAMPS") != nullptr;   // diagnostic only
+    if (want_stamps) {
+      if (!pl->d_stamps) HIP_TRY(hipMalloc(&pl->d_stamps, sizeof(long long) * NSTAMP * pl->tiles));
+      HIP_TRY(hipMemsetAsync(pl->d_stamps, 0, sizeof(long long) * NSTAMP * pl->tiles, st));
+      k.stamps = pl->d_stamps;
+    }
+    HIP_TRY(hipEventRecord(pl->ev0, st));
+    if (!pl->d_kp) HIP_TRY(hipMalloc(&pl->d_kp, sizeof(KParams)));
+    HIP_TRY(hipMemcpyAsync(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch(false, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, st));
+    HIP_TRY(hipEventRecord(pl->ev1, st));
+    pl->last_draws = dst;
+    pl->launched = true;
+    pl->ran = false;
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_plan_poll(fitoct_plan* pl, int64_t* iterations_done, int64_t* iterations_total,
                          int32_t* finished) {
-  if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
-  const int C = pl->kp.chains;
-  int64_t done = 0;
-  if (pl->h_prog)
-    for (int c = 0; c < C; ++c) done += __atomic_load_n(&pl->h_prog[c], __ATOMIC_RELAXED);
-  const int64_t total = (int64_t)C * (pl->kp.warmup + pl->kp.samples);
-  int32_t fin = pl->ran ? 1 : 0;
-  if (pl->launched) {
-    HIP_TRY(hipSetDevice(pl->cfg.device));
-    const hipError_t q = hipEventQuery(pl->ev1);
-    if (q == hipSuccess) fin = 1;
-    else if (q != hipErrorNotReady) HIP_TRY(q);
-  }
-  if (iterations_done) *iterations_done = (pl->h_prog || !fin) ? done : total;
-  if (iterations_total) *iterations_total = total;
-  if (finished) *finished = fin;
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    const int C = pl->kp.chains;
+    int64_t done = 0;
+    if (pl->h_prog)
+      for (int c = 0; c < C; ++c) done += __atomic_load_n(&pl->h_prog[c], __ATOMIC_RELAXED);
+    const int64_t total = (int64_t)C * (pl->kp.warmup + pl->kp.samples);
+    int32_t fin = pl->ran ? 1 : 0;
+    if (pl->launched) {
+      HIP_TRY(hipSetDevice(pl->cfg.device));
+      const hipError_t q = hipEventQuery(pl->ev1);
+      if (q == hipSuccess) fin = 1;
+      else if (q != hipErrorNotReady) HIP_TRY(q);
+    }
+    if (iterations_done) *iterations_done = (pl->h_prog || !fin) ? done : total;
+    if (iterations_total) *iterations_total = total;
+    if (finished) *finished = fin;
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_plan_cancel(fitoct_plan* pl) {
-  if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
-  if (!pl->h_cancel) return fail(FITOCT_E_ARG, "this plan has no cancellation flag (batch plan)");
-  __atomic_store_n(pl->h_cancel, 1, __ATOMIC_SEQ_CST);
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    if (!pl->h_cancel) return fail(FITOCT_E_ARG, "this plan has no cancellation flag (batch plan)");
+    __atomic_store_n(pl->h_cancel, 1, __ATOMIC_SEQ_CST);
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_plan_wait(fitoct_plan* pl) {
-  if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
-  if (!pl->launched) return pl->ran ? FITOCT_OK : fail(FITOCT_E_ARG, "plan has not been launched");
-  HIP_TRY(hipSetDevice(pl->cfg.device));
-  pl->launched = false;
-  HIP_TRY(hipEventSynchronize(pl->ev1));
-  float ms = 0.f;
-  HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
-  pl->kernel_ms = ms;
-  if (pl->d_stamps && getenv("FITOCT_STAMPS") != nullptr) {
-    std::vector<long long> h((size_t)NSTAMP * pl->tiles);
-    HIP_TRY(hipMemcpy(h.data(), pl->d_stamps, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
-    double steps = 0, tg = 0, tn = 0, tt = 0, smax = 0, tw = 0, nw = 0, tsw = 0, tno = 0;
-    double ts0 = 0, ts1 = 0;
-    double act_t[18] = {0}, act_n[18] = {0};
-    for (int t = 0; t < pl->tiles; ++t) {
-      const long long* o = h.data() + (size_t)NSTAMP * t;
-      steps += o[0];
-      tg += o[1];
-      tn += o[2];
-      tt += o[3];
-      tw += o[40];
-      nw += o[41];
-      tsw += o[42];
-      tno += o[43];
-      ts0 += o[44];
-      ts1 += o[45];
-      smax = std::max(smax, (double)o[0]);
-      for (int a = 0; a < 18; ++a) {
-        act_t[a] += o[4 + a];
-        act_n[a] += o[22 + a];
+  return guarded(__func__, [&]() -> int32_t {
+    if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    if (!pl->launched) return pl->ran ? FITOCT_OK : fail(FITOCT_E_ARG, "plan has not been launched");
+    HIP_TRY(hipSetDevice(pl->cfg.device));
+    pl->launched = false;
+    HIP_TRY(hipEventSynchronize(pl->ev1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
+    pl->kernel_ms = ms;
+    if (pl->d_stamps && getenv("FITOCT_STAMPS") != nullptr) {
+      std::vector<long long> h((size_t)NSTAMP * pl->tiles);
+      HIP_TRY(hipMemcpy(h.data(), pl->d_stamps, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
+      double steps = 0, tg = 0, tn = 0, tt = 0, smax = 0, tw = 0, nw = 0, tsw = 0, tno = 0;
+      double ts0 = 0, ts1 = 0;
+      double act_t[18] = {0}, act_n[18] = {0};
+      for (int t = 0; t < pl->tiles; ++t) {
+        const long long* o = h.data() + (size_t)NSTAMP * t;
+        steps += o[0];
+        tg += o[1];
+        tn += o[2];
+        tt += o[3];
+        tw += o[40];
+        nw += o[41];
+        tsw += o[42];
+        tno += o[43];
+        ts0 += o[44];
+        ts1 += o[45];
+        smax = std::max(smax, (double)o[0]);
+        for (int a = 0; a < 18; ++a) {
+          act_t[a] += o[4 + a];
+          act_n[a] += o[22 + a];
+        }
       }
+      double subt[12] = {0}, wb[8] = {0};
+      for (int t = 0; t < pl->tiles; ++t) {
+        for (int k = 0; k < 8; ++k) subt[k] += h[(size_t)NSTAMP * t + 48 + k];
+        for (int k = 0; k < 8; ++k) wb[k] += h[(size_t)NSTAMP * t + 56 + k];
+      }
+      fprintf(stderr, "[fitoct stamps] gradient-wave busy per sweep by wave:");
+      for (int k = 0; k < 8; ++k) fprintf(stderr, " %.0f", wb[k] / std::max(steps, 1.0));
+      fprintf(stderr, "\n");
+      fprintf(stderr, "[fitoct stamps] sub-action cycles per leaf (chain 0): ");
+      for (int k = 0; k < 12; ++k)
+        if (subt[k] > 0) fprintf(stderr, "s%d:%.0f ", k, subt[k] / std::max(act_n[11], 1.0));
+      fprintf(stderr, "\n");
+      fprintf(stderr, "[fitoct stamps] per action (chain 0 of each tile): ");
+      for (int a = 1; a < 18; ++a)
+        if (act_n[a] > 0) fprintf(stderr, "a%d:%.0fx%.0f ", a, act_n[a] / pl->tiles, act_t[a] / act_n[a]);
+      fprintf(stderr, "\n");
+      fprintf(stderr,
+              "[fitoct stamps] tiles=%d mean sweeps/tile=%.0f max=%.0f | per sweep: grad-wave busy %.0f "
+              "nuts-wave busy %.0f wall %.0f memtime ticks\n",
+              pl->tiles, steps / pl->tiles, smax, tg / steps, tn / steps, tt / steps);
+      fprintf(stderr,
+              "[fitoct stamps] chain 0 per NUTS round: busy %.0f, waiting for its gradient %.0f "
+              "(enqueue->sweep done %.0f, sweep done->resumed %.0f)\n",
+              tn / std::max(nw, 1.0), tw / std::max(nw, 1.0), tsw / std::max(nw, 1.0),
+              tno / std::max(nw, 1.0));
+      fprintf(stderr, "[fitoct stamps] enqueue -> first wave starts %.0f, last wave starts %.0f\n",
+              ts0 / std::max(nw, 1.0), ts1 / std::max(nw, 1.0));
     }
-    double subt[12] = {0}, wb[8] = {0};
-    for (int t = 0; t < pl->tiles; ++t) {
-      for (int k = 0; k < 8; ++k) subt[k] += h[(size_t)NSTAMP * t + 48 + k];
-      for (int k = 0; k < 8; ++k) wb[k] += h[(size_t)NSTAMP * t + 56 + k];
-    }
-    fprintf(stderr, "[fitoct stamps] gradient-wave busy per sweep by wave:");
-    for (int k = 0; k < 8; ++k) fprintf(stderr, " %.0f", wb[k] / std::max(steps, 1.0));
-    fprintf(stderr, "\n");
-    fprintf(stderr, "[fitoct stamps] sub-action cycles per leaf (chain 0): ");
-    for (int k = 0; k < 12; ++k)
-      if (subt[k] > 0) fprintf(stderr, "s%d:%.0f ", k, subt[k] / std::max(act_n[11], 1.0));
-    fprintf(stderr, "\n");
-    fprintf(stderr, "[fitoct stamps] per action (chain 0 of each tile): ");
-    for (int a = 1; a < 18; ++a)
-      if (act_n[a] > 0) fprintf(stderr, "a%d:%.0fx%.0f ", a, act_n[a] / pl->tiles, act_t[a] / act_n[a]);
-    fprintf(stderr, "\n");
-    fprintf(stderr,
-            "[fitoct stamps] tiles=%d mean sweeps/tile=%.0f max=%.0f | per sweep: grad-wave busy %.0f "
-            "nuts-wave busy %.0f wall %.0f memtime ticks\n",
-            pl->tiles, steps / pl->tiles, smax, tg / steps, tn / steps, tt / steps);
-    fprintf(stderr,
-            "[fitoct stamps] chain 0 per NUTS round: busy %.0f, waiting for its gradient %.0f "
-            "(enqueue->sweep done %.0f, sweep done->resumed %.0f)\n",
-            tn / std::max(nw, 1.0), tw / std::max(nw, 1.0), tsw / std::max(nw, 1.0),
-            tno / std::max(nw, 1.0));
-    fprintf(stderr, "[fitoct stamps] enqueue -> first wave starts %.0f, last wave starts %.0f\n",
-            ts0 / std::max(nw, 1.0), ts1 / std::max(nw, 1.0));
-  }
-  pl->ran = true;
-  return FITOCT_OK;
+    pl->ran = true;
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
-  const int32_t rc = fitoct_plan_launch(pl, d_draws, stream);
-  return rc ? rc : fitoct_plan_wait(pl);
+  return guarded(__func__, [&]() -> int32_t {
+    const int32_t rc = fitoct_plan_launch(pl, d_draws, stream);
+    return rc ? rc : fitoct_plan_wait(pl);
+  });
 }
 
 
 int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
-  if (!pl || !res) return fail(FITOCT_E_ARG, "NULL argument");
-  if (!pl->ran) return fail(FITOCT_E_ARG, "plan has not run");
-  HIP_TRY(hipSetDevice(pl->cfg.device));
-  const KParams& k = pl->kp;
-  const int C = k.chains, D = k.D;
-  res->n_cols = k.ncols;
-  res->iters_saved = k.iters_saved;
-  res->dim = D;
-  res->kernel_ms = pl->kernel_ms;
-  res->migrations = 0;
-  if (pl->d_mig) HIP_TRY(hipMemcpy(&res->migrations, pl->d_mig + MIG_MOVES, sizeof(int),
-                                   hipMemcpyDeviceToHost));
-  if (res->draws) {
-    const int64_t need = (int64_t)C * k.iters_saved * k.ncols;
-    if (res->draws_capacity < need) return fail(FITOCT_E_ARG, "draws buffer too small");
-    HIP_TRY(hipMemcpy(res->draws, pl->last_draws, pl->draws_bytes, hipMemcpyDeviceToHost));
-  }
-  if (res->stepsize) HIP_TRY(hipMemcpy(res->stepsize, k.fin_eps, sizeof(double) * C, hipMemcpyDeviceToHost));
-  if (res->inv_metric)
-    HIP_TRY(hipMemcpy(res->inv_metric, k.fin_minv, sizeof(double) * C * D, hipMemcpyDeviceToHost));
-  if (res->last_q) HIP_TRY(hipMemcpy(res->last_q, k.fin_q, sizeof(double) * C * D, hipMemcpyDeviceToHost));
-  std::vector<int> st(C);
-  HIP_TRY(hipMemcpy(st.data(), k.chain_status, sizeof(int) * C, hipMemcpyDeviceToHost));
-  if (res->chain_status) memcpy(res->chain_status, st.data(), sizeof(int) * C);
-  std::vector<long long> lf(C);
-  HIP_TRY(hipMemcpy(lf.data(), k.leapfrogs, sizeof(long long) * C, hipMemcpyDeviceToHost));
-  long long tot = 0;
-  for (long long v : lf) tot += v;
-  res->total_leapfrogs = tot;
-  for (int c = 0; c < C; ++c)
-    if (st[c] != 0) {
-      return fail(st[c], "chain " + std::to_string(k.chain_offset + c) + " failed with status " +
-                             std::to_string(st[c]));
+  return guarded(__func__, [&]() -> int32_t {
+    if (!pl || !res) return fail(FITOCT_E_ARG, "NULL argument");
+    if (!pl->ran) return fail(FITOCT_E_ARG, "plan has not run");
+    HIP_TRY(hipSetDevice(pl->cfg.device));
+    const KParams& k = pl->kp;
+    const int C = k.chains, D = k.D;
+    res->n_cols = k.ncols;
+    res->iters_saved = k.iters_saved;
+    res->dim = D;
+    res->kernel_ms = pl->kernel_ms;
+    res->migrations = 0;
+    if (pl->d_mig) HIP_TRY(hipMemcpy(&res->migrations, pl->d_mig + MIG_MOVES, sizeof(int),
+                                     hipMemcpyDeviceToHost));
+    if (res->draws) {
+      const int64_t need = (int64_t)C * k.iters_saved * k.ncols;
+      if (res->draws_capacity < need) return fail(FITOCT_E_ARG, "draws buffer too small");
+      HIP_TRY(hipMemcpy(res->draws, pl->last_draws, pl->draws_bytes, hipMemcpyDeviceToHost));
     }
-  return FITOCT_OK;
+    if (res->stepsize) HIP_TRY(hipMemcpy(res->stepsize, k.fin_eps, sizeof(double) * C, hipMemcpyDeviceToHost));
+    if (res->inv_metric)
+      HIP_TRY(hipMemcpy(res->inv_metric, k.fin_minv, sizeof(double) * C * D, hipMemcpyDeviceToHost));
+    if (res->last_q) HIP_TRY(hipMemcpy(res->last_q, k.fin_q, sizeof(double) * C * D, hipMemcpyDeviceToHost));
+    std::vector<int> st(C);
+    HIP_TRY(hipMemcpy(st.data(), k.chain_status, sizeof(int) * C, hipMemcpyDeviceToHost));
+    if (res->chain_status) memcpy(res->chain_status, st.data(), sizeof(int) * C);
+    std::vector<long long> lf(C);
+    HIP_TRY(hipMemcpy(lf.data(), k.leapfrogs, sizeof(long long) * C, hipMemcpyDeviceToHost));
+    long long tot = 0;
+    for (long long v : lf) tot += v;
+    res->total_leapfrogs = tot;
+    for (int c = 0; c < C; ++c)
+      if (st[c] != 0) {
+        return fail(st[c], "chain " + std::to_string(k.chain_offset + c) + " failed with status " +
+                               std::to_string(st[c]));
+      }
+    return FITOCT_OK;
+  });
 }
 
 void fitoct_plan_destroy(fitoct_plan* pl) { free_plan(pl); }
 
 int32_t fitoct_expgp_sample(const fitoct_problem* prob, const fitoct_config* cfg,
                             fitoct_result* res) {
-  const auto t0 = std::chrono::steady_clock::now();
-  fitoct_plan* pl = nullptr;
-  int rc = fitoct_plan_create(prob, cfg, &pl);
-  if (rc) return rc;
-  rc = fitoct_plan_run(pl, nullptr, nullptr);
-  if (!rc && res) rc = fitoct_plan_download(pl, res);
-  free_plan(pl);
-  if (res)
-    res->wall_ms =
-        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  return rc;
+  return guarded(__func__, [&]() -> int32_t {
+    const auto t0 = std::chrono::steady_clock::now();
+    fitoct_plan* pl = nullptr;
+    int rc = fitoct_plan_create(prob, cfg, &pl);
+    if (rc) return rc;
+    rc = fitoct_plan_run(pl, nullptr, nullptr);
+    if (!rc && res) rc = fitoct_plan_download(pl, res);
+    free_plan(pl);
+    if (res)
+      res->wall_ms =
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+  });
 }
 
 int32_t fitoct_split_rhat_ess(const double* x, int32_t chains, int32_t n, double* rhat,
                               double* ess) {
-  if (!x) return fail(FITOCT_E_ARG, "x is NULL");
-  return split_rhat_ess(x, chains, n, rhat, ess);
+  return guarded(__func__, [&]() -> int32_t {
+    if (!x) return fail(FITOCT_E_ARG, "x is NULL");
+    return split_rhat_ess(x, chains, n, rhat, ess);
+  });
 }
 
 int32_t fitoct_rank_rhat(const double* x, int32_t chains, int32_t n, double* rhat) {
-  if (!x || !rhat) return fail(FITOCT_E_ARG, "NULL argument");
-  return rank_rhat(x, chains, n, rhat);
+  return guarded(__func__, [&]() -> int32_t {
+    if (!x || !rhat) return fail(FITOCT_E_ARG, "NULL argument");
+    return rank_rhat(x, chains, n, rhat);
+  });
 }
 
 }  // extern "C"
@@ -1011,134 +1036,140 @@ extern "C" {
 
 int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
                             const fitoct_config* cfg, fitoct_batch** out) {
-  if (!out) return fail(FITOCT_E_ARG, "out is NULL");
-  *out = nullptr;
-  if (!probs || n_problems < 1) return fail(FITOCT_E_ARG, "need n_problems >= 1 problems");
-  if (!cfg) return fail(FITOCT_E_ARG, "config is NULL");
-  if (cfg->chains < 1) return fail(FITOCT_E_ARG, "chains must be >= 1");
-  if ((int64_t)n_problems * cfg->chains > (int64_t)1 << 30)
-    return fail(FITOCT_E_ARG, "too many chains in one batch");
-  fitoct_batch* b = new fitoct_batch();
-  b->cfg = *cfg;
-  const int C = cfg->chains;
-  auto build = [&]() -> int {
-    for (int p = 0; p < n_problems; ++p) {
-      if (probs[p].prior_type != probs[0].prior_type || probs[p].Nn != probs[0].Nn)
-        return fail(FITOCT_E_ARG, "batch problems must share prior_type and Nn (problem " +
-                                      std::to_string(p) + ")");
-      fitoct_config c = *cfg;
-      c.chain_offset = cfg->chain_offset + p * C;
-      fitoct_plan* pl = nullptr;
-      const int rc = plan_create(&probs[p], &c, n_problems * C, -1, &pl);
-      if (rc) return fail(rc, "problem " + std::to_string(p) + ": " + fitoct_last_error());
-      b->plans.push_back(pl);
-    }
-    // one kernel instantiation and one LDS carve must serve every problem
-    int bpt = 0;
-    for (fitoct_plan* pl : b->plans) bpt = std::max(bpt, pl->bpt == 0 ? 1 << 20 : pl->bpt);
-    const fitoct_plan* p0 = b->plans[0];
-    for (fitoct_plan* pl : b->plans) {
-      if (pl->kp.mode != p0->kp.mode || pl->nnp != p0->nnp || pl->ppl != p0->ppl ||
-          pl->mixed != p0->mixed || pl->kp.G != p0->kp.G)
-        return fail(FITOCT_E_ARG, "batch problems plan to different kernels (basis mode)");
-    }
-    // bins: every tile runs the batch's widest bin layout.  A problem planned with
-    // fewer bins per lane is restaged at the common n_pad (zero-weight padding).
-    if (bpt == 1 << 20) bpt = 0;
-    auto restage = [&](int to) -> int {
-      for (size_t p = 0; p < b->plans.size(); ++p) {
-        fitoct_plan* pl = b->plans[p];
-        if (pl && pl->bpt == to) continue;
+  return guarded(__func__, [&]() -> int32_t {
+    if (!out) return fail(FITOCT_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (!probs || n_problems < 1) return fail(FITOCT_E_ARG, "need n_problems >= 1 problems");
+    if (!cfg) return fail(FITOCT_E_ARG, "config is NULL");
+    if (cfg->chains < 1) return fail(FITOCT_E_ARG, "chains must be >= 1");
+    if ((int64_t)n_problems * cfg->chains > (int64_t)1 << 30)
+      return fail(FITOCT_E_ARG, "too many chains in one batch");
+    std::unique_ptr<fitoct_batch, void (*)(fitoct_batch*)> guard(new fitoct_batch(), free_batch);
+    fitoct_batch* b = guard.get();
+    b->cfg = *cfg;
+    const int C = cfg->chains;
+    auto build = [&]() -> int {
+      for (int p = 0; p < n_problems; ++p) {
+        if (probs[p].prior_type != probs[0].prior_type || probs[p].Nn != probs[0].Nn)
+          return fail(FITOCT_E_ARG, "batch problems must share prior_type and Nn (problem " +
+                                        std::to_string(p) + ")");
         fitoct_config c = *cfg;
-        c.chain_offset = cfg->chain_offset + (int)p * C;
-        free_plan(pl);
-        b->plans[p] = nullptr;
-        const int rc = plan_create(&probs[p], &c, n_problems * C, to, &b->plans[p]);
-        if (rc) return rc;
+        c.chain_offset = cfg->chain_offset + p * C;
+        fitoct_plan* pl = nullptr;
+        const int rc = plan_create(&probs[p], &c, n_problems * C, -1, &pl);
+        if (rc) return fail(rc, "problem " + std::to_string(p) + ": " + fitoct_last_error());
+        b->plans.push_back(pl);
       }
+      // one kernel instantiation and one LDS carve must serve every problem
+      int bpt = 0;
+      for (fitoct_plan* pl : b->plans) bpt = std::max(bpt, pl->bpt == 0 ? 1 << 20 : pl->bpt);
+      const fitoct_plan* p0 = b->plans[0];
+      for (fitoct_plan* pl : b->plans) {
+        if (pl->kp.mode != p0->kp.mode || pl->nnp != p0->nnp || pl->ppl != p0->ppl ||
+            pl->mixed != p0->mixed || pl->kp.G != p0->kp.G)
+          return fail(FITOCT_E_ARG, "batch problems plan to different kernels (basis mode)");
+      }
+      // bins: every tile runs the batch's widest bin layout.  A problem planned with
+      // fewer bins per lane is restaged at the common n_pad (zero-weight padding).
+      if (bpt == 1 << 20) bpt = 0;
+      auto restage = [&](int to) -> int {
+        for (size_t p = 0; p < b->plans.size(); ++p) {
+          fitoct_plan* pl = b->plans[p];
+          if (pl && pl->bpt == to) continue;
+          fitoct_config c = *cfg;
+          c.chain_offset = cfg->chain_offset + (int)p * C;
+          free_plan(pl);
+          b->plans[p] = nullptr;
+          const int rc = plan_create(&probs[p], &c, n_problems * C, to, &b->plans[p]);
+          if (rc) return rc;
+        }
+        return FITOCT_OK;
+      };
+      int rc = restage(bpt);
+      // the 16-bin layout needs an arithmetic depth grid in every problem: else stream all
+      if (rc && bpt == 16) rc = restage(0);
+      if (rc) return rc;
+      b->per_bytes = b->plans[0]->draws_bytes;
+      std::vector<int> map;
+      const int G = b->plans[0]->kp.G;
+      for (int p = 0; p < n_problems; ++p)
+        for (int c0 = 0; c0 < C; c0 += G) {
+          map.push_back(p);
+          map.push_back(c0);
+        }
+      b->tiles = (int)map.size() / 2;
+      HIP_TRY(hipSetDevice(cfg->device));
+      HIP_TRY(hipMalloc(&b->d_map, sizeof(int) * map.size()));
+      HIP_TRY(hipMemcpy(b->d_map, map.data(), sizeof(int) * map.size(), hipMemcpyHostToDevice));
+      HIP_TRY(hipMalloc(&b->d_kp, sizeof(KParams) * n_problems));
+      HIP_TRY(hipEventCreate(&b->ev0));
+      HIP_TRY(hipEventCreate(&b->ev1));
       return FITOCT_OK;
     };
-    int rc = restage(bpt);
-    // the 16-bin layout needs an arithmetic depth grid in every problem: else stream all
-    if (rc && bpt == 16) rc = restage(0);
+    const int rc = build();
     if (rc) return rc;
-    b->per_bytes = b->plans[0]->draws_bytes;
-    std::vector<int> map;
-    const int G = b->plans[0]->kp.G;
-    for (int p = 0; p < n_problems; ++p)
-      for (int c0 = 0; c0 < C; c0 += G) {
-        map.push_back(p);
-        map.push_back(c0);
-      }
-    b->tiles = (int)map.size() / 2;
-    HIP_TRY(hipSetDevice(cfg->device));
-    HIP_TRY(hipMalloc(&b->d_map, sizeof(int) * map.size()));
-    HIP_TRY(hipMemcpy(b->d_map, map.data(), sizeof(int) * map.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&b->d_kp, sizeof(KParams) * n_problems));
-    HIP_TRY(hipEventCreate(&b->ev0));
-    HIP_TRY(hipEventCreate(&b->ev1));
+    *out = guard.release();
     return FITOCT_OK;
-  };
-  const int rc = build();
-  if (rc) {
-    free_batch(b);
-    return rc;
-  }
-  *out = b;
-  return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_batch_get_info(const fitoct_batch* b, fitoct_plan_info* info) {
-  if (!b || !info) return fail(FITOCT_E_ARG, "NULL argument");
-  const int rc = fitoct_plan_get_info(b->plans[0], info);
-  if (rc) return rc;
-  info->chains = b->cfg.chains * (int)b->plans.size();
-  info->tiles = b->tiles;
-  info->draws_bytes = (int64_t)(b->per_bytes * b->plans.size());
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    if (!b || !info) return fail(FITOCT_E_ARG, "NULL argument");
+    const int rc = fitoct_plan_get_info(b->plans[0], info);
+    if (rc) return rc;
+    info->chains = b->cfg.chains * (int)b->plans.size();
+    info->tiles = b->tiles;
+    info->draws_bytes = (int64_t)(b->per_bytes * b->plans.size());
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
-  if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
-  HIP_TRY(hipSetDevice(b->cfg.device));
-  const size_t P = b->plans.size();
-  double* dst = (double*)d_draws;
-  if (!dst) {
-    if (!b->d_draws) HIP_TRY(hipMalloc(&b->d_draws, b->per_bytes * P));
-    dst = b->d_draws;
-  }
-  hipStream_t st = (hipStream_t)stream;
-  std::vector<KParams> kp(P);
-  for (size_t p = 0; p < P; ++p) {
-    fitoct_plan* pl = b->plans[p];
-    kp[p] = pl->kp;
-    kp[p].draws = (double*)((char*)dst + b->per_bytes * p);
-    pl->last_draws = kp[p].draws;
-    HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * pl->kp.chains, st));
-  }
-  HIP_TRY(hipMemcpyAsync(b->d_kp, kp.data(), sizeof(KParams) * P, hipMemcpyHostToDevice, st));
-  const fitoct_plan* p0 = b->plans[0];
-  HIP_TRY(hipEventRecord(b->ev0, st));
-  HIP_TRY(launch(false, p0->mixed, p0->bpt, p0->nnp, kp[0], b->d_kp, b->tiles, st, b->d_map));
-  HIP_TRY(hipEventRecord(b->ev1, st));
-  HIP_TRY(hipEventSynchronize(b->ev1));
-  float ms = 0.f;
-  HIP_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
-  b->kernel_ms = ms;
-  for (fitoct_plan* pl : b->plans) {
-    pl->kernel_ms = ms;
-    pl->ran = true;
-  }
-  b->ran = true;
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
+    HIP_TRY(hipSetDevice(b->cfg.device));
+    const size_t P = b->plans.size();
+    double* dst = (double*)d_draws;
+    if (!dst) {
+      if (!b->d_draws) HIP_TRY(hipMalloc(&b->d_draws, b->per_bytes * P));
+      dst = b->d_draws;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    std::vector<KParams> kp(P);
+    for (size_t p = 0; p < P; ++p) {
+      fitoct_plan* pl = b->plans[p];
+      kp[p] = pl->kp;
+      kp[p].draws = (double*)((char*)dst + b->per_bytes * p);
+      pl->last_draws = kp[p].draws;
+      HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * pl->kp.chains, st));
+    }
+    HIP_TRY(hipMemcpyAsync(b->d_kp, kp.data(), sizeof(KParams) * P, hipMemcpyHostToDevice, st));
+    const fitoct_plan* p0 = b->plans[0];
+    HIP_TRY(hipEventRecord(b->ev0, st));
+    HIP_TRY(launch(false, p0->mixed, p0->bpt, p0->nnp, kp[0], b->d_kp, b->tiles, st, b->d_map));
+    HIP_TRY(hipEventRecord(b->ev1, st));
+    HIP_TRY(hipEventSynchronize(b->ev1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    b->kernel_ms = ms;
+    for (fitoct_plan* pl : b->plans) {
+      pl->kernel_ms = ms;
+      pl->ran = true;
+    }
+    b->ran = true;
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_batch_download(fitoct_batch* b, int32_t problem, fitoct_result* res) {
-  if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
-  if (problem < 0 || problem >= (int32_t)b->plans.size())
-    return fail(FITOCT_E_ARG, "problem index out of range");
-  if (!b->ran) return fail(FITOCT_E_ARG, "batch has not run");
-  return fitoct_plan_download(b->plans[problem], res);
+  return guarded(__func__, [&]() -> int32_t {
+    if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
+    if (problem < 0 || problem >= (int32_t)b->plans.size())
+      return fail(FITOCT_E_ARG, "problem index out of range");
+    if (!b->ran) return fail(FITOCT_E_ARG, "batch has not run");
+    return fitoct_plan_download(b->plans[problem], res);
+  });
 }
 
 void fitoct_batch_destroy(fitoct_batch* b) { free_batch(b); }

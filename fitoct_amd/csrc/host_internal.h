@@ -1,5 +1,7 @@
 // Internal declarations shared by the host translation units of libfitoct.
 #pragma once
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -18,5 +20,20 @@ int rank_rhat(const double* x, int chains, int n, double* out);
 bool log_transformed(int prior, int Nn, int j);
 void constrain(int prior, int Nn, const double* q, double* out);
 double lp_constant(const fitoct_problem* p);
+
+// Every extern "C" entry that can allocate runs its body through guarded(): no C++
+// exception crosses the ABI (include/fitoct.h); a failure becomes a status + message.
+template <class F>
+int guarded(const char* fn, F&& body) noexcept {
+  try {
+    return body();
+  } catch (const std::bad_alloc&) {
+    return fail(FITOCT_E_INTERNAL, std::string(fn) + ": out of host memory");
+  } catch (const std::exception& e) {
+    return fail(FITOCT_E_INTERNAL, std::string(fn) + ": " + e.what());
+  } catch (...) {
+    return fail(FITOCT_E_INTERNAL, std::string(fn) + ": unknown exception");
+  }
+}
 
 }  // namespace fitoct

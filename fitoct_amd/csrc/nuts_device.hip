@@ -302,7 +302,9 @@ __device__ __forceinline__ XF xf_norm(double m, int e) {
 }
 __device__ __forceinline__ XF xf_exp(double x) {   // exp(x), x <= +inf; -inf -> 0
   if (x > -700.0 && x < 700.0) return xf_norm(fexp(x), 0);
-  if (!(x > -INFINITY)) return XF{0.0, 0};
+  // below -1e9 (a divergent leaf: its weight is never merged) the exponent would not fit
+  // an int; the weight is 0 to every digit the merges can resolve
+  if (!(x > -1.0e9)) return XF{0.0, 0};
   const double k = floor(x * 1.4426950408889634);   // log2(e)
   return xf_norm(fexp(fma(-k, 0.6931471805599453, x)), (int)k);
 }

@@ -136,37 +136,43 @@ using namespace fitoct;
 extern "C" {
 
 int32_t fitoct_output_n_params(const fitoct_problem* prob) {
-  if (check_layout_problem(prob)) return -1;
-  return (int32_t)out_layout(prob).size();
+  return guarded(__func__, [&]() -> int32_t {
+    if (check_layout_problem(prob)) return -1;
+    return (int32_t)out_layout(prob).size();
+  });
 }
 
 int32_t fitoct_output_param_name(const fitoct_problem* prob, int32_t i, char* buf, int32_t buflen) {
-  int rc = check_layout_problem(prob);
-  if (rc) return rc;
-  const std::vector<OutCol> lay = out_layout(prob);
-  if (i < 0 || i >= (int32_t)lay.size()) return fail(FITOCT_E_ARG, "output column index out of range");
-  const std::string& s = lay[i].name;
-  if (!buf || buflen < (int32_t)s.size() + 1) return fail(FITOCT_E_ARG, "buffer too small");
-  memcpy(buf, s.c_str(), s.size() + 1);
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    int rc = check_layout_problem(prob);
+    if (rc) return rc;
+    const std::vector<OutCol> lay = out_layout(prob);
+    if (i < 0 || i >= (int32_t)lay.size()) return fail(FITOCT_E_ARG, "output column index out of range");
+    const std::string& s = lay[i].name;
+    if (!buf || buflen < (int32_t)s.size() + 1) return fail(FITOCT_E_ARG, "buffer too small");
+    memcpy(buf, s.c_str(), s.size() + 1);
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_output_rows(const fitoct_problem* prob, int32_t n_lead, int64_t n_rows,
                            const double* raw, double* out) {
-  int rc = check_layout_problem(prob);
-  if (rc) return rc;
-  if (n_lead < 0 || n_rows < 0 || (n_rows > 0 && (!raw || !out)))
-    return fail(FITOCT_E_ARG, "bad buffers");
-  const std::vector<OutCol> lay = out_layout(prob);
-  const int D = model_dim(prob->prior_type, prob->Nn);
-  const int64_t w_in = n_lead + D + 1, w_out = n_lead + (int64_t)lay.size();
-  for (int64_t r = 0; r < n_rows; ++r) {
-    const double* src = raw + r * w_in;
-    double* dst = out + r * w_out;
-    for (int j = 0; j < n_lead; ++j) dst[j] = src[j];
-    fill_row(prob, lay, src + n_lead, dst + n_lead);
-  }
-  return FITOCT_OK;
+  return guarded(__func__, [&]() -> int32_t {
+    int rc = check_layout_problem(prob);
+    if (rc) return rc;
+    if (n_lead < 0 || n_rows < 0 || (n_rows > 0 && (!raw || !out)))
+      return fail(FITOCT_E_ARG, "bad buffers");
+    const std::vector<OutCol> lay = out_layout(prob);
+    const int D = model_dim(prob->prior_type, prob->Nn);
+    const int64_t w_in = n_lead + D + 1, w_out = n_lead + (int64_t)lay.size();
+    for (int64_t r = 0; r < n_rows; ++r) {
+      const double* src = raw + r * w_in;
+      double* dst = out + r * w_out;
+      for (int j = 0; j < n_lead; ++j) dst[j] = src[j];
+      fill_row(prob, lay, src + n_lead, dst + n_lead);
+    }
+    return FITOCT_OK;
+  });
 }
 
 int32_t fitoct_write_stan_csv(const char* path, const fitoct_problem* prob,

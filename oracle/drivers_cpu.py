@@ -14,7 +14,7 @@ import os
 
 from . import nuts_c
 
-LIB = os.path.join(nuts_c.HERE, "build", "libdrivers_cpu.so")
+LIB = os.path.join(nuts_c.BUILD_DIR, "libdrivers_cpu.so")
 _L = None
 NAMES = ("fitoct_optimize", "fitoct_vb", "fitoct_default_optim_config",
          "fitoct_default_vb_config", "fitoct_evaluator_create", "fitoct_evaluator_run",

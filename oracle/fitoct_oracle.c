@@ -394,7 +394,9 @@ static xf xf_norm(double m, int e) {
 }
 static xf xf_exp(double x) {
   if (x > -700.0 && x < 700.0) return xf_norm(exp(x), 0);
-  if (!(x > -INFINITY)) {
+  /* below -1e9 (a divergent leaf, never merged) the exponent would overflow an int
+   * (UBSan, scripts/cpu_sanitized_suite.sh); the weight is 0 to every resolvable digit */
+  if (!(x > -1.0e9)) {
     xf z = {0.0, 0};
     return z;
   }

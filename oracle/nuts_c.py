@@ -13,7 +13,10 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "liboracle.so")
+# FITOCT_SANITIZE=1: the ASan/UBSan build (make -C oracle sanitize) in oracle/build_san/
+SANITIZE = os.environ.get("FITOCT_SANITIZE", "0") not in ("", "0")
+BUILD_DIR = os.path.join(HERE, "build_san" if SANITIZE else "build")
+LIB = os.path.join(BUILD_DIR, "liboracle.so")
 _L = None
 
 
@@ -24,7 +27,8 @@ def build(force: bool = False) -> str:
     """make -C oracle (once per process; make tracks the sources)."""
     global _BUILT
     if force or not _BUILT:
-        subprocess.run(["make", "-s", "-C", HERE] + (["-B"] if force else []), check=True)
+        subprocess.run(["make", "-s", "-C", HERE] + (["sanitize"] if SANITIZE else [])
+                       + (["-B"] if force else []), check=True)
         _BUILT = True
     return LIB
 

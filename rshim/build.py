@@ -10,8 +10,13 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "src", "fitoct_drive.c")
-OUT = os.path.join(HERE, "libfitoct_drive.so")
-LIBDIR = os.path.join(ROOT, "fitoct_amd")
+# FITOCT_SANITIZE=1 (scripts/cpu_sanitized_suite.sh): an ASan/UBSan driver linked to the
+# sanitized libfitoct (fitoct_amd/build_san/), so both share one library instance
+SANITIZE = os.environ.get("FITOCT_SANITIZE", "0") not in ("", "0")
+OUT = os.path.join(HERE, "build_san", "libfitoct_drive.so") if SANITIZE else \
+    os.path.join(HERE, "libfitoct_drive.so")
+LIBDIR = os.path.join(ROOT, "fitoct_amd", "build_san") if SANITIZE else \
+    os.path.join(ROOT, "fitoct_amd")
 
 
 def build(force: bool = False) -> str:
@@ -21,9 +26,13 @@ def build(force: bool = False) -> str:
     newest = max(os.path.getmtime(p) for p in (SRC, SRC[:-1] + "h", lib))
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= newest:
         return OUT
-    cmd = ["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", "-Werror", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), SRC, "-o", OUT,
-           "-L", LIBDIR, "-lfitoct", "-Wl,-rpath,$ORIGIN/../fitoct_amd"]
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    cc = ["/opt/rocm/lib/llvm/bin/clang", "-fsanitize=address,undefined", "-shared-libsan",
+          "-g"] if SANITIZE else ["gcc"]
+    rpath = "$ORIGIN/../../fitoct_amd/build_san" if SANITIZE else "$ORIGIN/../fitoct_amd"
+    cmd = cc + ["-std=c99", "-O2", "-Wall", "-Wextra", "-Werror", "-fPIC", "-shared",
+                "-I", os.path.join(ROOT, "include"), SRC, "-o", OUT,
+                "-L", LIBDIR, "-lfitoct", f"-Wl,-rpath,{rpath}"]
     subprocess.run(cmd, check=True)
     return OUT
 

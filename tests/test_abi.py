@@ -200,3 +200,19 @@ def test_degenerate_inputs_rejected(case):
     with pytest.raises(_lib.FitOCTError) as ei:
         logp_grad(prob, np.zeros((1, prob.D)))
     assert ei.value.code == -1 and len(str(ei.value)) > 0
+
+
+def test_oversize_n_rejected():
+    """N above FITOCT_MAX_BINS (include/fitoct.h) fails with FITOCT_E_ARG before any
+    allocation sized by N, with or without a device."""
+    hdr = open(HEADER).read()
+    max_bins = eval(re.search(r"#define FITOCT_MAX_BINS \((.*)\)", hdr).group(1))
+    from fitoct_amd.api import logp_grad
+    x = np.linspace(20.0, 500.0, max_bins + 1)
+    prob = ExpGPProblem(x, 1000.0 + 0 * x, 1.0 + 0 * x, Nn=5)
+    with pytest.raises(_lib.FitOCTError) as ei:
+        logp_grad(prob, np.zeros((1, prob.D)))
+    assert ei.value.code == -1 and "FITOCT_MAX_BINS" in str(ei.value)
+    out = np.empty(3)
+    assert _lib.lib().fitoct_mono_initial_theta(max_bins + 1, _lib.dptr(x), _lib.dptr(x), 2,
+                                                _lib.dptr(out)) == -1

@@ -59,6 +59,8 @@ def test_deterministic_and_seed_sensitive():
 
 
 @pytest.mark.parametrize("path", golden_files("draws"), ids=lambda p: os.path.basename(p))
+@pytest.mark.skipif(nuts_c.SANITIZE, reason="the fixture pins the gcc -O3 -march=x86-64-v3 "
+                    "build's arithmetic; the sanitized oracle is clang -O1")
 def test_oracle_reproduces_draw_fixture(path):
     fx = load_golden(path)
     m = fx["meta"]
