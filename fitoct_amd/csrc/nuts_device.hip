@@ -3,23 +3,25 @@
 // Replaces rstan::sampling + Stan's base_nuts / adapt_diag_e_nuts + the
 // stanc-generated model with stan-math AD.
 //
-// Execution model ("tile" = one 768-thread workgroup, persistent for the whole run):
+// Execution model ("tile" = one 512-thread workgroup of 8 waves, persistent for the
+// whole run; kernel_params.h NW / NGW / GMAX):
 //   * a tile owns G <= 4 chains.  Each chain is an explicit state machine (init
 //     -> step-size search -> tree building -> adaptation -> next transition)
 //     that consumes one gradient per leapfrog, so a chain that finishes its
 //     trajectory starts its next transition at once: no chain waits for
 //     another chain's tree.
-//   * the 12 waves are specialised: waves 0..7 only run the likelihood sweep,
-//     waves 8..11 only run NUTS (one chain each), so neither role's registers
-//     are live in the other's code.  The roles meet in a dataflow pipeline
-//     through LDS: a NUTS wave enqueues its chain's next position in a ring,
-//     the gradient waves drain the ring in order and count their completions
-//     per chain, the NUTS wave resumes when all 8 sweeps are in.  No barrier
-//     after start-up: each chain's sampler latency hides behind the sweeps of
-//     the tile's other chains.
-//   * gradient waves: the N depth bins are strided over 512 lanes; each lane
-//     keeps its bins' data resident in VGPRs for the
-//     whole run (read from HBM once per tile, shared by all G chains).  For the
+//   * the 8 waves are specialised: waves 0..3 only run the likelihood sweep,
+//     waves 4..7 only run NUTS (one chain each); waves w and w+4 share SIMD
+//     w mod 4, so every SIMD holds one gradient wave and one NUTS wave.  The
+//     roles meet in a dataflow pipeline through LDS: a NUTS wave enqueues its
+//     chain's next position in a ring, the gradient waves drain the ring in
+//     order and count their completions per chain, the NUTS wave resumes when
+//     all 4 sweeps are in.  No barrier after start-up: each chain's sampler
+//     latency hides behind the sweeps of the tile's other chains.
+//   * gradient waves: the N depth bins are strided over 256 lanes; each lane
+//     keeps its bins' data resident in VGPRs for the whole run (read from HBM
+//     once per tile, shared by all G chains; up to 8 bins per lane, or 16 in
+//     the compact layout for arithmetic depth grids).  For the
 //     built-in uniform-grid SE basis (MODE_POLY) the GP basis factorises as
 //     K(x~_i, g_l) = a_i t_i^l b_l, so a bin needs 5 registers (c*x, y, 1/uy,
 //     t, a) instead of a 16-wide basis row: dL_i = a_i P(t_i) by Horner on the
@@ -28,17 +30,18 @@
 //     rows in registers (MODE_ROWS, fp32) or streams them (MODE_STREAM).
 //     Per chain a lane accumulates 4+NNP partial sums; a transposed butterfly
 //     built from v_permlane32_swap / v_permlane16_swap / DPP row mirrors
-//     reduces them across the wave (no LDS round trips), and 8 per-wave
+//     reduces them across the wave (no LDS round trips), and 4 per-wave
 //     partials land in LDS.
-//   * NUTS phase (wave c drives chain c): lane k holds parameter k.  The wave
-//     sums the 8 partials, completes lp / grad with the priors and the
+//   * NUTS phase (wave 4+c drives chain c): lane k holds parameter k.  The wave
+//     sums the 4 partials, completes lp / grad with the priors and the
 //     log-Jacobians, and advances the chain's state machine.  Stan's recursive
 //     build_tree is replayed iteratively, one leaf per step: the U-turn records
 //     (p_beg, p_end, rho) of each tree level live in LDS, the multinomial
 //     proposals (q, p, grad) in a per-chain HBM pool addressed by slot index, so
 //     a proposal is written once when its leaf is pushed and read only when it
 //     becomes the sample.  Wave reductions are DPP/permlane butterflies.
-//   * no inter-workgroup communication at all.
+//   * workgroups communicate only to hand whole chains between tiles at transition
+//     boundaries (chain migration, the MIG instantiation).
 //
 // Random numbers are addressable Philox draws (philox.h), identical to the CPU
 // oracle's, so short horizons of GPU and CPU chains coincide draw for draw.

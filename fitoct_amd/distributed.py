@@ -46,9 +46,11 @@ def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=N
     returns the full :class:`SampleOutput` (chains in global order), other ranks
     return their local output without draws.
 
-    ``engine(prob, local_cfg) -> SampleOutput`` runs one shard on the host side
-    (used with ``gloo``); with the ``nccl`` backend the HIP plan writes draws into
-    a device tensor that is gathered over RCCL directly.
+    Without ``engine`` each rank's HIP plan writes its draws into a device tensor;
+    with the ``nccl`` backend that tensor is gathered over RCCL directly, with
+    ``gloo`` (ranks sharing a GPU in tests and rehearsals) through a host copy.
+    ``engine(prob, local_cfg) -> SampleOutput`` replaces the plan by a host-side
+    sampler (the CPU tests run the C oracle this way).
     """
     import torch
     import torch.distributed as dist
@@ -60,7 +62,7 @@ def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=N
         raise ValueError(f"rank {rank} has no chains ({cfg.chains} chains over {world} ranks)")
     local = replace(cfg, chains=count, chain_offset=cfg.chain_offset + offset)
     nccl = dist.get_backend() == "nccl"
-    if nccl:
+    if engine is None:
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         local = replace(local, device=dev.index)
         with Plan(prob, local) as pl:
@@ -69,9 +71,10 @@ def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=N
             buf = torch.zeros((cmax, iters, ncols), dtype=torch.float64, device=dev)
             pl.run(d_draws=buf.data_ptr(), stream=torch.cuda.current_stream(dev).cuda_stream)
             out = pl.download(with_draws=False)
+        if not nccl:          # gloo gathers host tensors
+            torch.cuda.current_stream(dev).synchronize()
+            buf, dev = buf.cpu(), torch.device("cpu")
     else:
-        if engine is None:
-            from .api import sample as engine
         out = engine(prob, local)
         iters, ncols = out.draws.shape[1:]
         buf = torch.zeros((cmax, iters, ncols), dtype=torch.float64)
@@ -108,9 +111,9 @@ def sample_batch_sharded(probs, cfg: SamplerConfig, engine=None, device=None):
     a single batch of all files.  Rank 0 returns one :class:`SampleOutput` per file
     (global file order); other ranks return their local outputs.
 
-    ``engine(prob, cfg) -> SampleOutput`` samples one file on the host side (used
-    with ``gloo``); with ``nccl`` the batch writes its draws into a device tensor
-    that is gathered over RCCL.
+    Without ``engine`` the batch writes its draws into a device tensor, gathered over
+    RCCL with ``nccl`` and through a host copy with ``gloo``; ``engine(prob, cfg) ->
+    SampleOutput`` samples one file on the host side instead (CPU tests).
     """
     import torch
     import torch.distributed as dist
@@ -127,7 +130,7 @@ def sample_batch_sharded(probs, cfg: SamplerConfig, engine=None, device=None):
     local = replace(cfg, chain_offset=cfg.chain_offset + off * C)
     mine = probs[off:off + cnt]
     nccl = dist.get_backend() == "nccl"
-    if nccl:
+    if engine is None:
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         local = replace(local, device=dev.index)
         with Batch(mine, local) as b:
@@ -135,9 +138,10 @@ def sample_batch_sharded(probs, cfg: SamplerConfig, engine=None, device=None):
             buf = torch.zeros((fmax, C, iters, ncols), dtype=torch.float64, device=dev)
             b.run(d_draws=buf.data_ptr(), stream=torch.cuda.current_stream(dev).cuda_stream)
             outs = [b.download(p, with_draws=False) for p in range(cnt)]
+        if not nccl:          # gloo gathers host tensors
+            torch.cuda.current_stream(dev).synchronize()
+            buf, dev = buf.cpu(), torch.device("cpu")
     else:
-        if engine is None:
-            from .api import sample as engine
         outs = [engine(p, replace(local, chain_offset=local.chain_offset + i * C))
                 for i, p in enumerate(mine)]
         iters, ncols = outs[0].draws.shape[1:]

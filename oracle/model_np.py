@@ -26,7 +26,8 @@ The flagged (⚑) assumptions of Appendix A are explicit keyword switches here
 (``kernel_conv``, ``lambda_conv``, ``sigma_scale``, ``nugget``) and carry the
 same meaning in the C oracle and in the HIP library.
 
-What pins it instead: analytic prior-only known answers (tests/test_oracle_kat.py),
+What pins it instead: analytic prior-only known answers (tests/kat_cases.py, run by
+tests/test_oracle_nuts.py and tests/test_gpu_sampler.py),
 finite-difference gradient checks, and the golden vectors this file generates
 (tests/golden/make_golden.py).
 """

@@ -1,8 +1,10 @@
-"""Chain sharding over a process group (gloo, world_size 2, CPU): the gathered
-draws on rank 0 equal a single-process run of all chains, for even and uneven
-splits.  The engine on each rank is the C oracle (the GPU path is the same code
-with the nccl backend and the HIP plan; covered on the GPU box by
-tests/test_gpu_sampler.py::test_sharded_plan_matches_single_plan)."""
+"""Chain sharding over a process group (gloo, world_size 2): the gathered draws on
+rank 0 equal a single-process run of all chains, for even and uneven splits.
+
+CPU: the engine on each rank is the C oracle.  GPU (``-m gpu``): both ranks run the
+HIP plan on cuda:0 into device buffers -- the code path the nccl backend takes on a
+node, with the one collective done through a host copy because RCCL refuses two
+ranks on one device -- and the gathered draws equal a single plan bit for bit."""
 from __future__ import annotations
 
 import os
@@ -120,3 +122,61 @@ def test_gloo_world2_batch_files_equal_single_runs(tmp_path):
         ref = _oracle_engine(prob, SamplerConfig(chains=2, warmup=20, samples=10, seed=5,
                                                  max_treedepth=4, chain_offset=2 * f))
         np.testing.assert_array_equal(got["draws"][f], ref.draws)
+
+
+def _hip_worker(rank, world, port, chains, outdir, batch):
+    import torch
+    import torch.distributed as dist
+    from fitoct_amd.api import SamplerConfig
+    from fitoct_amd.distributed import sample_batch_sharded, sample_sharded
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        if batch:
+            cfg = SamplerConfig(chains=2, warmup=20, samples=10, seed=5, max_treedepth=5)
+            outs = sample_batch_sharded(_batch_problems(), cfg)
+            if rank == 0:
+                np.savez(os.path.join(outdir, "gathered.npz"),
+                         draws=np.stack([o.draws for o in outs]))
+        else:
+            cfg = SamplerConfig(chains=chains, warmup=60, samples=40, seed=21, max_treedepth=6)
+            out = sample_sharded(_gpu_problem(), cfg)
+            if rank == 0:
+                np.savez(os.path.join(outdir, "gathered.npz"), draws=out.draws,
+                         stepsize=out.stepsize, lf=out.total_leapfrogs)
+    finally:
+        dist.destroy_process_group()
+
+
+def _gpu_problem():
+    from fitoct_amd import ExpGPProblem
+    from fitoct_amd.synth import default_prior, synth_decay
+    t0, S0 = default_prior()
+    d = synth_decay(512, "sincExp2", 9)
+    return ExpGPProblem(d["x"], d["y"], d["uy"], Nn=10, gridType="extremal", theta0=t0,
+                        Sigma0=S0, prior_type="horseshoe")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chains", [64, 37])
+def test_hip_plan_sharded_gather_equals_single_plan(tmp_path, chains):
+    from fitoct_amd.api import SamplerConfig, sample
+    mp.spawn(_hip_worker, args=(2, _free_port(), chains, str(tmp_path), False), nprocs=2,
+             join=True)
+    got = np.load(tmp_path / "gathered.npz")
+    ref = sample(_gpu_problem(), SamplerConfig(chains=chains, warmup=60, samples=40, seed=21,
+                                               max_treedepth=6))
+    np.testing.assert_array_equal(got["draws"], ref.draws)
+    np.testing.assert_array_equal(got["stepsize"], ref.stepsize)
+    assert int(got["lf"]) == ref.total_leapfrogs
+
+
+@pytest.mark.gpu
+def test_hip_batch_sharded_gather_equals_single_batch(tmp_path):
+    from fitoct_amd.api import SamplerConfig, sample_batch
+    mp.spawn(_hip_worker, args=(2, _free_port(), 0, str(tmp_path), True), nprocs=2, join=True)
+    got = np.load(tmp_path / "gathered.npz")["draws"]
+    ref = sample_batch(_batch_problems(), SamplerConfig(chains=2, warmup=20, samples=10, seed=5,
+                                                        max_treedepth=5))
+    np.testing.assert_array_equal(got, np.stack([o.draws for o in ref]))
