@@ -19,21 +19,18 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
+    """Build libfitoct.so (hipcc cross-compiles without a GPU) and the C oracle
+    before collection -- test modules load the library at import time, and a
+    rebuild after that would leave two instances of it in the process (the R-shim
+    driver binds the rebuilt file).  Incremental in the build container; on the GPU
+    box (gpurun exports GRAFT_REPO_ROOT) only if missing: it uses the prebuilt files."""
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X)")
     config.addinivalue_line("markers", "slow: long-running test")
-
-
-@pytest.fixture(scope="session", autouse=True)
-def _built_library():
-    """Build libfitoct.so (hipcc cross-compiles without a GPU) and the C oracle:
-    incrementally in the build container, only if missing on the GPU box
-    (gpurun exports GRAFT_REPO_ROOT there), which uses the prebuilt files."""
     from fitoct_amd import build as B
     if not os.path.exists(B.LIB) or not os.environ.get("GRAFT_REPO_ROOT"):
         B.build()
     from oracle import nuts_c
     nuts_c.build()
-    yield
 
 
 def golden_files(prefix):
