@@ -1130,15 +1130,25 @@ struct Chain {
   __device__ int act_grad() {
     FITOCT_MARK(act_grad);
     long long ts = stamp0();
+    const int stt = uni(Sp->state);
     V g;
     double s0;
+    if (stt == ST_TREE) {
+      // the leaf's position, momentum and the metric are read while the bin sums reduce
+      const V q = ld(V_CUR_Q), p = ld(V_CUR_P), minv = ld(V_MINV);
+      const double lp = finish_grad(g, s0);
+      sub(4, ts);
+      st(V_CUR_G, g);
+      Sp->cur_lp = lp;
+      Sp->cur_s2 = s0;
+      return leaf(q, p, g, minv, lp, s0);
+    }
     const double lp = finish_grad(g, s0);
     sub(4, ts);
     st(V_CUR_G, g);
     Sp->cur_lp = lp;
     Sp->cur_s2 = s0;
-    const int stt = uni(Sp->state);
-    return stt == ST_TREE ? A_LEAF : stt == ST_STEPSIZE ? A_SS_STEP : A_INIT_STEP;
+    return stt == ST_STEPSIZE ? A_SS_STEP : A_INIT_STEP;
   }
 
   __device__ int act_init_state() {
@@ -1237,9 +1247,12 @@ struct Chain {
   // A_LEAPFROG: begin_update_p + update_q from CUR with step Sp->lf_e
   __device__ int act_leapfrog() {
     FITOCT_MARK(act_leapfrog);
-    const double e = Sp->lf_e;
-    V q = ld(V_CUR_Q), p = ld(V_CUR_P);
-    const V g = ld(V_CUR_G), minv = ld(V_MINV);
+    return leapfrog_stage(ld(V_CUR_Q), ld(V_CUR_P), ld(V_CUR_G), ld(V_MINV), Sp->lf_e);
+  }
+  // begin_update_p + update_q from (q, p, g) in registers, then stage the new position
+  // for the gradient waves (write_mp): the whole path to the next sweep without an LDS
+  // round trip or an action dispatch
+  __device__ int leapfrog_stage(V q, V p, const V& g, const V& minv, const double e) const {
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       p.a[s] = fma(0.5 * e, g.a[s], p.a[s]);        // p -= e/2 dphi/dq
@@ -1247,7 +1260,8 @@ struct Chain {
     }
     st(V_CUR_P, p);
     st(V_CUR_Q, q);
-    return A_WRITE_MP;
+    write_mp(q);
+    return A_YIELD;
   }
   __device__ int act_write_mp() {
     FITOCT_MARK(act_write_mp);
@@ -1349,24 +1363,23 @@ struct Chain {
     const int dir = (u > 0.5) ? 1 : 0;
     Sp->dir = dir;
     const int eq = dir ? V_E1_Q : V_E0_Q;
-    const V pe = ld(eq + 1);
+    const V qe = ld(eq), pe = ld(eq + 1), ge = ld(eq + 2), minv = ld(V_MINV);
     st(V_PNEAR, pe);
-    copyv(V_CUR_Q, eq);
-    st(V_CUR_P, pe);
-    copyv(V_CUR_G, eq + 2);
+    st(V_CUR_G, ge);
     Sp->cur_lp = Sp->end_lp[dir];
     Sp->cur_s2 = Sp->end_s2[dir];
     Sp->leaf = 0;
-    Sp->lf_e = dir ? Sp->eps_used : -Sp->eps_used;
-    return A_LEAPFROG;
+    const double e = dir ? Sp->eps_used : -Sp->eps_used;
+    Sp->lf_e = e;
+    return leapfrog_stage(qe, pe, ge, minv, e);   // act_leapfrog + act_write_mp
   }
 
   // proposal pool: at most max_depth + 1 live slots (stack records + the running
   // subtree).  `used` is the slot bitmask, kept in registers by the caller.
-  __device__ int pool_put(unsigned& used, const V& p, double lp, double s2) const {
+  __device__ int pool_put(unsigned& used, const V& q, const V& p, const V& g, double lp,
+                          double s2) const {
     const int sl = __builtin_ctz(~used);
     used |= 1u << sl;
-    const V q = ld(V_CUR_Q), g = ld(V_CUR_G);
     AS_GLB double* dq = pslot(sl, P_Q);
     AS_GLB double* dp = pslot(sl, P_P);
     AS_GLB double* dg = pslot(sl, P_G);
@@ -1385,15 +1398,19 @@ struct Chain {
   // when the subtree of depth d is complete, the top-level merge of the transition.
   // Chain scalars are read once into registers and written back once, so the
   // action costs a handful of LDS round trips instead of one per field.
-  __device__ int act_leaf() {
+  // Reached from act_grad (state ST_TREE) with the leaf's q, p (begin-updated), the
+  // gradient just completed, the metric, lp and sum r^2 in registers.  A leaf inside
+  // the subtree continues straight into the next leapfrog and stages its position
+  // (act_leapfrog + act_write_mp with the same arithmetic, no LDS round trip or
+  // dispatch between them).
+  __device__ int leaf(const V& q, V p, const V& g, const V& minv, const double cur_lp,
+                      const double cur_s2) {
     FITOCT_MARK(act_leaf);
     long long ts = stamp0();
-    const double e = Sp->lf_e, cur_lp = Sp->cur_lp, cur_s2 = Sp->cur_s2, H0 = Sp->H0;
+    const double e = Sp->lf_e, H0 = Sp->H0;
     const double sum_metro0 = Sp->sum_metro;
     const int d = uni(Sp->depth), j = uni(Sp->leaf), nlf = uni(Sp->n_leapfrog);
     unsigned used = (unsigned)uni(Sp->pool_used);
-    V p = ld(V_CUR_P);
-    const V g = ld(V_CUR_G), minv = ld(V_MINV);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) p.a[s] = fma(0.5 * e, g.a[s], p.a[s]);   // end_update_p
     st(V_CUR_P, p);
@@ -1421,7 +1438,7 @@ struct Chain {
         lst(l, K_RHO, Trho);
         Sp->st_w_m[l] = Tw.m;
         Sp->st_w_e[l] = Tw.e;
-        Sp->st_prop[l] = (Tprop < 0) ? pool_put(used, p, cur_lp, cur_s2) : Tprop;
+        Sp->st_prop[l] = (Tprop < 0) ? pool_put(used, q, p, g, cur_lp, cur_s2) : Tprop;
         break;
       }
       // merge init I = level l with final T (base_nuts::build_tree at depth l+1)
@@ -1457,14 +1474,14 @@ struct Chain {
     if (j != (1 << d) - 1) {
       Sp->pool_used = (int)used;
       Sp->leaf = j + 1;
-      return A_LEAPFROG;
+      return leapfrog_stage(q, p, g, minv, e);   // act_leapfrog + act_write_mp
     }
     // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
     const int dir = uni(Sp->dir);
     const XF Ww{Sp->lsw_m, Sp->lsw_e};
     const double u_top = Sp->u_top;
     const int eq = dir ? V_E1_Q : V_E0_Q;
-    copyv(eq, V_CUR_Q);
+    st(eq, q);
     st(eq + 1, p);
     st(eq + 2, g);
     Sp->end_lp[dir] = cur_lp;
@@ -1473,7 +1490,7 @@ struct Chain {
     const bool take = xf_gt(Tw, Ww) || xf_u_below(u_top, Tw, Ww);   // u_top: drawn by act_prior
     if (take) {
       if (Tprop < 0) {
-        copyv(V_SMP_Q, V_CUR_Q);
+        st(V_SMP_Q, q);
         st(V_SMP_P, p);
         st(V_SMP_G, g);
         Sp->smp_lp = cur_lp;
@@ -1745,7 +1762,6 @@ struct Chain {
         case A_SS_FINISH: a = act_ss_finish(); break;
         case A_START_TRANSITION: a = act_start_transition(); break;
         case A_BEGIN_SUBTREE: a = act_begin_subtree(); break;
-        case A_LEAF: a = act_leaf(); break;
         case A_END_TREE: a = act_end_tree(); break;
         case A_NEXT_TRANSITION: a = act_next_transition(); break;
         case A_FINISH: a = act_finish(); break;
