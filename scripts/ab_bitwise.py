@@ -1,6 +1,6 @@
 """Bitwise A/B of variant libraries: every abtest/lib_*.so samples the same short
 runs (configs 2, 3, 4 shapes and a batch of config-5 files), and each variant's draws
-are compared bit for bit with abtest/lib_base.so.  Latency-only changes (same
+are compared bit for bit (SHA-256 of the draw arrays) with abtest/lib_base.so.  Latency-only changes (same
 arithmetic) must print 'identical'.
 
     python scripts/ab_bitwise.py            # on the GPU box
@@ -36,7 +36,9 @@ for f in range(16):
                               Sigma0=S0, prior_type="normal"))
 outs = sample_batch(probs, SamplerConfig(chains=4, warmup=60, samples=40, seed=9))
 res["c5"] = np.stack([o.draws for o in outs])
-np.savez(sys.argv[1], **res)
+import hashlib, json
+json.dump({k: hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() for k, v in res.items()},
+          open(sys.argv[1], "w"))
 """
 
 
@@ -46,20 +48,20 @@ def main():
     for lib in libs:
         name = os.path.basename(lib)[4:-3]
         env = dict(os.environ, FITOCT_LIB_PATH=lib)
-        r = subprocess.run([sys.executable, "-c", RUNNER % ROOT, os.path.join(OUT, name + ".npz")],
+        r = subprocess.run([sys.executable, "-c", RUNNER % ROOT, os.path.join(OUT, name + ".json")],
                            env=env, timeout=300)
         if r.returncode != 0:
             print(f"{name}: run failed ({r.returncode})", flush=True)
             return 1
-    base = np.load(os.path.join(OUT, "base.npz"))
+    import json
+    base = json.load(open(os.path.join(OUT, "base.json")))
     for lib in libs:
         name = os.path.basename(lib)[4:-3]
         if name == "base":
             continue
-        got = np.load(os.path.join(OUT, name + ".npz"))
-        for k in base.files:
-            same = np.array_equal(base[k], got[k], equal_nan=True)
-            print(f"{name} {k}: {'identical' if same else 'DIFFERENT'}", flush=True)
+        got = json.load(open(os.path.join(OUT, name + ".json")))
+        for k in base:
+            print(f"{name} {k}: {'identical' if base[k] == got[k] else 'DIFFERENT'}", flush=True)
     return 0
 
 
