@@ -412,6 +412,7 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   k.lambda_scale = p->lambda_scale;
   k.nu = p->nu;
   k.sigma_scale = p->sigma_scale;
+  k.sigma_scale_inv = 1.0 / p->sigma_scale;
   k.chains = chains;
 
   // chains per tile: fill every CU with one tile first, then stack chains
@@ -801,6 +802,7 @@ int32_t fitoct_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
       if (!pl->d_stamps) HIP_TRY(hipMalloc(&pl->d_stamps, sizeof(long long) * NSTAMP * pl->tiles));
       HIP_TRY(hipMemsetAsync(pl->d_stamps, 0, sizeof(long long) * NSTAMP * pl->tiles, st));
       k.stamps = pl->d_stamps;
+      k.bench_sweeps = getenv("FITOCT_BENCH_SWEEPS") ? atoi(getenv("FITOCT_BENCH_SWEEPS")) : 0;
     }
     HIP_TRY(hipEventRecord(pl->ev0, st));
     if (!pl->d_kp) HIP_TRY(hipMalloc(&pl->d_kp, sizeof(KParams)));

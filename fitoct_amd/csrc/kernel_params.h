@@ -66,6 +66,7 @@ struct KParams {
   double lambda_scale;      // lasso lambda_s
   double nu;                // horseshoe nu
   double sigma_scale;
+  double sigma_scale_inv;   // 1 / sigma_scale
   // ---- sampler ----
   int chains;               // chains in this launch
   int chain_offset;         // global id of chain 0
@@ -85,6 +86,9 @@ struct KParams {
   int* chain_status;        // [chains]
   long long* leapfrogs;     // [chains]
   long long* stamps;        // optional [tiles][4]: half-steps, gradient busy, NUTS busy, total cycles
+  int bench_sweeps;         // profiling build only (FITOCT_BENCH_SWEEPS): after the first
+                            // position, each chain re-enqueues it this many times and stops
+                            // (the sweep alone, no sampler work between sweeps)
   // ---- chain migration (nullptr / 0: off) ----
   int* mig;                 // MigCtrl header | load | free_mask | mailbox (see MigCtrl)
   double* mig_img;          // [tiles * GMAX][mig_img_words] chain images in flight

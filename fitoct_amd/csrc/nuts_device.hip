@@ -108,7 +108,7 @@ struct ChainScalars {
   double H0, lsw_m, sum_metro, eps, eps_used, mu, s_bar, x_bar, ss_H0, lf_e;
   double cur_lp, cur_s2, smp_lp, smp_s2;
   double pr_lp, pr_is2, u_top, pad4;
-  double u_merge[MAXDEPTH];
+  int u_blk[MAXDEPTH];     // which block of 64 merge uniforms each level's ring holds (-1: none)
   double end_lp[2], end_s2[2];
   double st_w_m[MAXDEPTH];
   double pool_lp[MAXDEPTH + 1], pool_s2[MAXDEPTH + 1];
@@ -605,7 +605,9 @@ struct Lds {
     return KBYTES + (GMAX * MPW + NGW * G * NSLOT) * 8;
   }
   static __host__ __device__ constexpr int chain_bytes(int max_depth) {
-    return (int)sizeof(ChainScalars) + (NVEC * VLEN + NSLOT + NAUX + max_depth * NLVL * VLEN) * 8;
+    // ... | levels[max_depth][NLVL][VLEN] | merge-uniform rings[max_depth][WAVE]
+    return (int)sizeof(ChainScalars) +
+           (NVEC * VLEN + NSLOT + NAUX + max_depth * NLVL * VLEN + max_depth * WAVE) * 8;
   }
   static __host__ __device__ constexpr int bytes(int G, int max_depth) {
     return head_bytes(G) + G * chain_bytes(max_depth);
@@ -736,6 +738,7 @@ struct Chain {
   AS_LDS double* SUMS;
   AS_LDS double* AUX;   // [0,32): yGP ; [32,64): horseshoe lambda_j * tau
   AS_LDS double* LV;    // [max_depth][NLVL][VLEN]
+  AS_LDS double* RNG;   // [max_depth][WAVE]: level l's merge uniforms, one block of 64 merges
   AS_LDS double* MP;
   AS_LDS double* part;
   const AS_LDS double* Kinv;
@@ -750,7 +753,8 @@ struct Chain {
 
   __device__ Chain(KPc& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
       : pp(&P_), Sp(&L.cs(slot_)), Vb(L.vecs(slot_)), SUMS(L.sums(slot_)), AUX(L.aux(slot_)),
-        LV(L.lvls(slot_)), MP(L.mp(slot_)), part(L.part()), Kinv(L.kinv()), bv(L.bv()),
+        LV(L.lvls(slot_)), RNG(L.lvls(slot_) + (size_t)P_.max_depth * NLVL * VLEN), MP(L.mp(slot_)),
+        part(L.part()), Kinv(L.kinv()), bv(L.bv()),
         lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
     gid = Pr().chain_offset + lc;
     key = make_key(Pr().seed, (uint32_t)gid);
@@ -933,13 +937,13 @@ struct Chain {
     const double Sd0 = Si[0] * d0 + Si[1] * d1 + Si[2] * d2;
     const double Sd1 = Si[3] * d0 + Si[4] * d1 + Si[5] * d2;
     const double Sd2t = Si[6] * d0 + Si[7] * d1 + Si[8] * d2;
-    const double ss = Pr().sigma_scale;
+    const double iss = Pr().sigma_scale_inv;   // 1 / sigma_scale (host division)
     const double gyf = lik ? th1 * th2 * is2 : 0.0;   // dlp/dyGP_k = gyf * S[4+k]
     double lpc = 0.0;
     if (lane == 0) {
       if (lik) lpc += -(double)Pr().N * usig;
       lpc += -0.5 * (d0 * Sd0 + d1 * Sd1 + d2 * Sd2t) + qs[0] + qs[1] + qs[2];
-      if (!mono) lpc += -0.5 * (sig / ss) * (sig / ss) + usig;
+      if (!mono) lpc += -0.5 * (sig * iss) * (sig * iss) + usig;
     }
     double ysum = 0.0;   // normal family: sum yGP^2
     if (fam == FAM_NORMAL) ysum = wave_sum(lane < Nn ? AUX[lane] * AUX[lane] : 0.0);
@@ -959,17 +963,19 @@ struct Chain {
         } else if (mono) {
           // no other parameter
         } else if (k == D - 1) {
-          gk = (lik ? -(double)Pr().N : 0.0) - sig * sig / (ss * ss) + 1.0;
+          gk = (lik ? -(double)Pr().N : 0.0) - (sig * iss) * (sig * iss) + 1.0;
           if (lik) ck = is2;
         } else if (fam == FAM_NORMAL) {
-          const double lam = qe[3 + Nn];
+          // one reciprocal for the wave (lambda is the same on every lane) instead of an
+          // IEEE division per term: no division latency on the sampler's path
+          const double lam = qe[3 + Nn], il2 = frcp(lam * lam);
           if (k < 3 + Nn) {
-            gk = -qk / (lam * lam);
+            gk = -qk * il2;
             ck = gyf;
-            lpc += -qk * qk / (2.0 * lam * lam);
-          } else {  // lambda
+            lpc += -0.5 * qk * qk * il2;
+          } else {  // lambda: lam * (-Nn / lam + ysum / lam^3 - rate) + 1
             const double rate = Pr().lambda_rate_eff;
-            gk = lam * (-(double)Nn / lam + ysum / (lam * lam * lam) - rate) + 1.0;
+            gk = -(double)Nn + ysum * il2 - rate * lam + 1.0;
             lpc += -(double)Nn * qk - rate * lam + qk;
           }
         } else if (fam == FAM_LASSO) {
@@ -1113,13 +1119,24 @@ struct Chain {
     long long ts = stamp0();
     prior_part();
     sub(7, ts);
-    if (uni(Sp->state) == ST_TREE) {   // one Philox per lane, all in parallel
+    if (uni(Sp->state) == ST_TREE) {
+      // The coming leaf j completes the merges of levels l < nm (trailing ones of j).
+      // The k-th level-l merge of a subtree sits at leaf (k + 1) 2^(l+1) - 1; each
+      // level keeps a ring of the uniforms of 64 consecutive merges, refilled a block
+      // at a time by one Philox per lane (same counters as one draw per merge, so the
+      // same numbers), i.e. one Philox pass per 64 merges instead of per leaf.
       const int d = uni(Sp->depth), j = uni(Sp->leaf);
       const uint32_t t = (uint32_t)uni(Sp->t);
-      const int nm = min(d, (int)__builtin_ctz(~(unsigned)j));   // merges: trailing ones of j
-      if (lane < nm)
-        Sp->u_merge[lane] = uniform(key, t, TAG_MERGE | ((uint32_t)lane << 8) |
-                                    ((uint32_t)d << 16), (uint32_t)j, 0u);
+      const int nm = min(d, (int)__builtin_ctz(~(unsigned)j));
+      for (int l = 0; l < nm; ++l) {
+        const int blk = (j >> (l + 1)) >> 6;
+        if (uni(Sp->u_blk[l]) != blk) {
+          const int jj = ((((blk << 6) + lane) + 1) << (l + 1)) - 1;   // may pass the subtree's end: unused
+          RNG[l * WAVE + lane] = uniform(key, t, TAG_MERGE | ((uint32_t)l << 8) | ((uint32_t)d << 16),
+                                         (uint32_t)jj, 0u);
+          if (lane == 0) Sp->u_blk[l] = blk;
+        }
+      }
       if (lane == WAVE - 1 && j == (1 << d) - 1)
         Sp->u_top = uniform(key, t, TAG_TOP, (uint32_t)d, 0u);
     }
@@ -1369,6 +1386,7 @@ struct Chain {
     Sp->cur_lp = Sp->end_lp[dir];
     Sp->cur_s2 = Sp->end_s2[dir];
     Sp->leaf = 0;
+    if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;   // merge uniforms are per subtree (depth d)
     const double e = dir ? Sp->eps_used : -Sp->eps_used;
     Sp->lf_e = e;
     return leapfrog_stage(qe, pe, ge, minv, e);   // act_leapfrog + act_write_mp
@@ -1444,7 +1462,7 @@ struct Chain {
       // merge init I = level l with final T (base_nuts::build_tree at depth l+1)
       const V Ipb = lld(l, K_PBEG), Ipe = lld(l, K_PEND), Irho = lld(l, K_RHO);
       const XF Iw{Sp->st_w_m[l], Sp->st_w_e[l]};
-      const double um = Sp->u_merge[l];   // drawn by act_prior
+      const double um = RNG[l * WAVE + ((j >> (l + 1)) & (WAVE - 1))];   // drawn by act_prior
       const int Iprop = uni(Sp->st_prop[l]);
       const XF Sw = xf_add(Iw, Tw);
       const bool take_final = xf_gt(Tw, Sw) || xf_u_below(um, Tw, Sw);
@@ -1803,6 +1821,12 @@ __device__ __forceinline__ unsigned long long lds_load64(const unsigned long lon
   return __atomic_load_n(p, __ATOMIC_RELAXED);
 }
 constexpr int RINGN = 16;                 // hand-off ring: >= 2 * GMAX entries
+#ifndef FITOCT_NUTS_POLL
+#define FITOCT_NUTS_POLL 1
+#endif
+#ifndef FITOCT_NUTS_WAIT_PRIO
+#define FITOCT_NUTS_WAIT_PRIO 0
+#endif
 constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded, never hang a box
 
 // Migration receiver: post NUTS slot c of this tile as free and wait until a
@@ -1997,9 +2021,22 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           in_sweep = false;
           long long spins = 0;
           const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
-          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
-            if (++spins > SPIN_LIMIT) break;
-            __builtin_amdgcn_s_sleep(1);
+          // A NUTS wave waits at priority 3 on a SIMD it shares with a gradient wave.  When
+          // the sweep is long (8+ bins per lane, or streamed bins) and the tile hosts
+          // several chains, the wait is long and the sampler is not the bottleneck: poll
+          // rarely, so the waiting wave leaves the SIMD's issue to the gradient wave.
+          if (P.G >= 2 && (BPT >= 8 || BPT == 0)) {
+            if (FITOCT_NUTS_WAIT_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_NUTS_WAIT_PRIO);
+            while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
+              if (++spins > SPIN_LIMIT) break;
+              __builtin_amdgcn_s_sleep(FITOCT_NUTS_POLL);
+            }
+            if (FITOCT_NUTS_WAIT_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
+          } else {
+            while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
+              if (++spins > SPIN_LIMIT) break;
+              __builtin_amdgcn_s_sleep(1);
+            }
           }
           if (stamp) {
             const long long t1 = (long long)__builtin_amdgcn_s_memtime();
@@ -2029,6 +2066,21 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           ch.Sp->status = ERR_TIMEOUT;
           a = Ch::A_FINISH;
           continue;
+        }
+        if constexpr (kProfile) {
+          if (P.bench_sweeps > 0 && P.stamps != nullptr) {   // sweep-only measurement
+            for (int r = 0; r < P.bench_sweeps; ++r) {
+              if (lane == 0) {
+                const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
+                __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
+                                 __ATOMIC_RELAXED);
+              }
+              ++epoch;
+              while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) __builtin_amdgcn_s_sleep(1);
+            }
+            ch.Sp->state = ST_DONE;
+            break;
+          }
         }
         // enqueue chain c: sequence number from a ring-wide counter, one 64-bit store
         if (lane == 0) {
