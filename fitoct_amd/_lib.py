@@ -69,6 +69,7 @@ class PlanInfo(C.Structure):
         ("chains", C.c_int32), ("tiles", C.c_int32), ("chains_per_tile", C.c_int32),
         ("bins_per_thread", C.c_int32), ("threads_per_tile", C.c_int32),
         ("lds_bytes", C.c_int32), ("n_pad", C.c_int32), ("draws_bytes", C.c_int64),
+        ("sampler", C.c_int32), ("reserved", C.c_int32),
     ]
 
 

@@ -427,6 +427,9 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   k.G = G;
   k.max_depth = max_depth;
   k.nuts_prio = getenv("FITOCT_NUTS_PRIO") ? atoi(getenv("FITOCT_NUTS_PRIO")) : 3;
+  // one chain per tile leaves three NUTS slots idle: one of them helps the chain's
+  // NUTS wave (speculative leaves, nuts_device.hip leaf_spec); FITOCT_NO_SPEC=1: off
+  k.spec = (G == 1 && getenv("FITOCT_NO_SPEC") == nullptr) ? 1 : 0;
   pl->tiles = (chains + G - 1) / G;
   pl->lds = lds_bytes(pl->ppl, G, max_depth);
   return FITOCT_OK;
@@ -769,6 +772,9 @@ int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
     info->chains = pl->kp.chains;
     info->tiles = pl->tiles;
     info->chains_per_tile = pl->kp.G;
+    info->sampler = pl->mig_bytes > 0 ? FITOCT_SAMPLER_MIGRATE
+                    : pl->kp.spec ? FITOCT_SAMPLER_SPECULATIVE : FITOCT_SAMPLER_PLAIN;
+    info->reserved = 0;
     info->bins_per_thread = pl->bpt;
     info->threads_per_tile = TPB;
     info->lds_bytes = pl->lds;
@@ -890,9 +896,11 @@ int32_t fitoct_plan_wait(fitoct_plan* pl) {
       fprintf(stderr, "[fitoct stamps] gradient-wave busy per sweep by wave:");
       for (int k = 0; k < 8; ++k) fprintf(stderr, " %.0f", wb[k] / std::max(steps, 1.0));
       fprintf(stderr, "\n");
-      fprintf(stderr, "[fitoct stamps] sub-action cycles per leaf (chain 0): ");
+      // per gradient of chain 0 (act_n[1]: A_GRAD runs); a11 is the speculative path's
+      // separate bookkeeping action (A_SPEC_BOOK)
+      fprintf(stderr, "[fitoct stamps] sub-action cycles per gradient (chain 0): ");
       for (int k = 0; k < 12; ++k)
-        if (subt[k] > 0) fprintf(stderr, "s%d:%.0f ", k, subt[k] / std::max(act_n[11], 1.0));
+        if (subt[k] > 0) fprintf(stderr, "s%d:%.0f ", k, subt[k] / std::max(act_n[1], 1.0));
       fprintf(stderr, "\n");
       fprintf(stderr, "[fitoct stamps] per action (chain 0 of each tile): ");
       for (int a = 1; a < 18; ++a)

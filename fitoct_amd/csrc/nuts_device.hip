@@ -64,6 +64,12 @@ namespace fitoct {
 using KPc = const AS_CST KParams;
 
 enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2, FAM_MONO = 3 };
+#ifndef FITOCT_EXP11
+#define FITOCT_EXP11 0
+#endif
+#ifndef FITOCT_RCP2
+#define FITOCT_RCP2 0
+#endif
 
 // Cycle stamps (FITOCT_STAMPS) exist only in a profiling build
 // (FITOCT_PROFILE=1 python -m fitoct_amd.build): the production kernels carry
@@ -367,6 +373,22 @@ template <> __device__ __forceinline__ double exp_<double>(double x) {
   const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
   double r = fma(-n, 6.93147180369123816490e-01, x);
   r = fma(-n, 1.90821492927058770002e-10, r);
+#if FITOCT_EXP11
+  // degree-11 Chebyshev fit on |r| <= ln2/2 (scripts/micro/exp_fit.py): <= 1 ulp from the
+  // correctly rounded exp, one FMA fewer than Taylor-12
+  double p = 2.5110037605963777e-08;
+  p = fma(p, r, 2.763263963904103e-07);
+  p = fma(p, r, 2.755724091857897e-06);
+  p = fma(p, r, 2.4801485482328494e-05);
+  p = fma(p, r, 0.00019841269890047113);
+  p = fma(p, r, 0.0013888888952314775);
+  p = fma(p, r, 0.008333333333319601);
+  p = fma(p, r, 0.0416666666664881);
+  p = fma(p, r, 0.1666666666666668);
+  p = fma(p, r, 0.5000000000000019);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+#else
   double p = 2.08767569878680989792e-09;   // 1/12!
   p = fma(p, r, 2.50521083854417187751e-08);
   p = fma(p, r, 2.75573192239858906526e-07);
@@ -380,6 +402,7 @@ template <> __device__ __forceinline__ double exp_<double>(double x) {
   p = fma(p, r, 0.5);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
+#endif
   return ldexp(p, ni);
 }
 template <> __device__ __forceinline__ float exp_<float>(float x) { return __expf(x); }
@@ -388,6 +411,20 @@ template <> __device__ __forceinline__ float exp_<float>(float x) { return __exp
 // acc: [0] sum d^2, [1] sum a, [2] sum a e, [3] sum w; returns h (adjoint seed of dL).
 // The non-physical guard (1 + dL <= 0 -> lp = -inf) is a per-lane running min
 // (umin), applied once after the lane's bins (no per-bin selects).
+template <class R, class A, int NA>
+__device__ __forceinline__ R bin_tail(R iL, R cx, R y, R isu, R th1, R th2, A (&acc)[NA]) {
+  const R e = exp_<R>(-cx * iL);                                 // exp(-c x / L)
+  const R m = fma(th2, e, th1);                                  // ui.R:88
+  const R d = (y - m) * isu;                                     // (y-m)/uy
+  const R a = d * isu;                                           // dlp/dm * sigma^2
+  const R ae = a * e;
+  const R w = ae * cx * iL;
+  acc[0] += (A)(d * d);
+  acc[1] += (A)a;
+  acc[2] += (A)ae;
+  acc[3] += (A)w;
+  return w * iL;                                                 // dlp/ddL / (th2 th3) * sigma^2
+}
 template <class R, class A, int NA>
 __device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th3, A (&acc)[NA],
                                       R& umin) {
@@ -434,6 +471,27 @@ __device__ __forceinline__ R bin_poly_fwd(R cx, R y, R isu, R t, R av, R th1, R 
 #pragma unroll
   for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
   return bin_core<R, A, 4 + NNP>(av * P, cx, y, isu, th1, th2, th3, acc, umin) * av;
+}
+
+// Two bins of bin_poly_fwd sharing one reciprocal: 1/L0 = L1 / (L0 L1), 1/L1 = L0 / (L0 L1)
+// (one quarter-rate v_rcp_f64 and its Newton step for two bins, <= 3 ulp).
+template <class R, int NNP, class A>
+__device__ __forceinline__ void bin_poly_fwd2(R cx0, R y0, R isu0, R t0, R a0, R cx1, R y1,
+                                              R isu1, R t1, R a1, R th1, R th2, R th3,
+                                              const R (&cf)[NNP], A (&acc)[4 + NNP], R& umin,
+                                              R& w0, R& w1) {
+  R P0 = cf[NNP - 1], P1 = cf[NNP - 1];
+#pragma unroll
+  for (int k = NNP - 2; k >= 0; --k) {
+    P0 = fma(P0, t0, cf[k]);
+    P1 = fma(P1, t1, cf[k]);
+  }
+  const R u0 = R(1) + a0 * P0, u1 = R(1) + a1 * P1;
+  umin = fmin(umin, fmin(u0, u1));
+  const R L0 = th3 * u0, L1 = th3 * u1;
+  const R ip = rcp_<R>(L0 * L1);
+  w0 = bin_tail<R, A, 4 + NNP>(ip * L1, cx0, y0, isu0, th1, th2, acc) * a0;
+  w1 = bin_tail<R, A, 4 + NNP>(ip * L0, cx1, y1, isu1, th1, th2, acc) * a1;
 }
 
 // Moments of one lane's BPT bins t_b = t0 R^b:  M_l = t0^l sum_b w_b (R^l)^b.
@@ -652,6 +710,17 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         double w[8];
+#if FITOCT_RCP2
+#pragma unroll
+        for (int b = 0; b < 8; b += 2) {
+          const int bb = half * 8 + b;
+          bin_poly_fwd2<R, NNP, double>(
+              cx0 + P.geo_dcx[bb], bins.y[bb], bins.isu[bb], fmin(t0 * P.geo_R[bb], tmax),
+              bins.row[bb][1], cx0 + P.geo_dcx[bb + 1], bins.y[bb + 1], bins.isu[bb + 1],
+              fmin(t0 * P.geo_R[bb + 1], tmax), bins.row[bb + 1][1], th1, th2, th3, cf, acc, umin,
+              w[b], w[b + 1]);
+        }
+#else
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
           const int bb = half * 8 + b;
@@ -660,15 +729,28 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
           w[b] = bin_poly_fwd<R, NNP, double>(cxb, bins.y[bb], bins.isu[bb], tb,
                                               bins.row[bb][1], th1, th2, th3, cf, acc, umin);
         }
+#endif
         moments_geo_add<8, NNP>(P, half ? t0 * P.geo_R[8] : t0, w, acc);
       }
     } else if constexpr (BPT > 0 && MODE == MODE_POLY && sizeof(R) == 8) {
       if (P.geo) {
         double w[BPT];
+#if FITOCT_RCP2
+        if constexpr (BPT % 2 == 0) {
 #pragma unroll
-        for (int b = 0; b < BPT; ++b)
-          w[b] = bin_poly_fwd<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
-                                              bins.row[b][1], th1, th2, th3, cf, acc, umin);
+          for (int b = 0; b < BPT; b += 2)
+            bin_poly_fwd2<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
+                                          bins.row[b][1], bins.cx[b + 1], bins.y[b + 1],
+                                          bins.isu[b + 1], bins.row[b + 1][0], bins.row[b + 1][1],
+                                          th1, th2, th3, cf, acc, umin, w[b], w[b + 1]);
+        } else
+#endif
+        {
+#pragma unroll
+          for (int b = 0; b < BPT; ++b)
+            w[b] = bin_poly_fwd<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
+                                                bins.row[b][1], th1, th2, th3, cf, acc, umin);
+        }
         moments_geo<BPT, NNP>(P, bins.row[0][0], w, acc);
       } else {
 #pragma unroll
@@ -728,7 +810,8 @@ struct Vd {
 // MIG = false: a sampler built without chain migration (plans where it cannot
 // run: one chain per tile, batch mode, FITOCT_NO_MIGRATE), so the receive loop
 // and the donor check cost no registers in the NUTS waves
-template <int PPL, int NNP, int FAM, bool MIG = true>
+// SPEC = true: speculative leaves with a helper wave (one chain per tile, no migration)
+template <int PPL, int NNP, int FAM, bool MIG = true, bool SPEC = false>
 struct Chain {
   using V = Vd<PPL>;
   static constexpr int VLEN = WAVE * PPL;
@@ -749,6 +832,12 @@ struct Chain {
   double krow[KROW ? NNP : 1];
   const AS_LDS double* bv;
   int lane, slot, lc, gid, nct;
+  bool spec;   // speculative leaves with a helper wave (KParams::spec: one chain per tile)
+  // a speculated leaf's values, kept from leaf_spec to act_spec_book (across the hand-off)
+  V k_q, k_pe, k_g, k_minv, k_ps, k_gs;
+  double k_lp, k_s2, k_en;
+  int k_dirn, k_dn, k_jn;
+  uint32_t k_t;
   RngKey key;
 
   __device__ Chain(KPc& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
@@ -757,6 +846,7 @@ struct Chain {
         part(L.part()), Kinv(L.kinv()), bv(L.bv()),
         lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
     gid = Pr().chain_offset + lc;
+    spec = SPEC && !MIG && nct_ == 1;
     key = make_key(Pr().seed, (uint32_t)gid);
     if constexpr (KROW) {
       const int r = lane < NNP ? lane : 0;
@@ -1094,8 +1184,14 @@ struct Chain {
   enum Act : int {
     A_YIELD = 0, A_GRAD, A_INIT_STATE, A_INIT_START, A_INIT_STEP, A_SS_BEGIN, A_SS_TRIAL,
     A_SS_STEP, A_SS_FINISH, A_START_TRANSITION, A_BEGIN_SUBTREE, A_LEAF, A_END_TREE,
-    A_NEXT_TRANSITION, A_FINISH, A_LEAPFROG, A_WRITE_MP, A_PRIOR
+    A_NEXT_TRANSITION, A_FINISH, A_LEAPFROG, A_WRITE_MP, A_PRIOR,
+    // the speculative path (leaf_spec): A_SPEC_STAGED yields a staged position for the
+    // kernel to enqueue and hand to the helper wave, A_SPEC_BOOK then does the leaf's
+    // bookkeeping and yields A_SPEC_WAIT (wait for the sweep and the helper, then A_GRAD)
+    // or A_SPEC_DISCARD (the trajectory ended: drain both, then A_END_TREE)
+    A_SPEC_STAGED, A_SPEC_BOOK, A_SPEC_WAIT, A_SPEC_DISCARD
   };
+  enum LeafBook : int { LB_MID = 0, LB_NEXT = 1, LB_END = 2 };
 
   __device__ __forceinline__ int uni(int x) const { return __builtin_amdgcn_readfirstlane(x); }
   // diagnostic sub-action stamps (profiling build + FITOCT_STAMPS): cycles since t
@@ -1116,17 +1212,24 @@ struct Chain {
   // part of lp / grad, and the uniforms the coming leaf's merges will consume
   __device__ int act_prior() {
     FITOCT_MARK(act_prior);
+    const bool tree = uni(Sp->state) == ST_TREE;
+    prior_and_uniforms(tree, uni(Sp->depth), uni(Sp->leaf), (uint32_t)uni(Sp->t));
+    return A_YIELD;
+  }
+  // The position-only part of lp / grad, and (tree building, leaf j of the subtree of
+  // depth d) the uniforms that leaf's merges will consume.  Run by the chain's NUTS
+  // wave (A_PRIOR) or, for a speculated leaf, by the tile's helper wave.
+  __device__ void prior_and_uniforms(const bool tree, const int d, const int j,
+                                     const uint32_t t) const {
     long long ts = stamp0();
     prior_part();
     sub(7, ts);
-    if (uni(Sp->state) == ST_TREE) {
-      // The coming leaf j completes the merges of levels l < nm (trailing ones of j).
+    if (tree) {
+      // Leaf j completes the merges of levels l < nm (trailing ones of j).
       // The k-th level-l merge of a subtree sits at leaf (k + 1) 2^(l+1) - 1; each
       // level keeps a ring of the uniforms of 64 consecutive merges, refilled a block
       // at a time by one Philox per lane (same counters as one draw per merge, so the
       // same numbers), i.e. one Philox pass per 64 merges instead of per leaf.
-      const int d = uni(Sp->depth), j = uni(Sp->leaf);
-      const uint32_t t = (uint32_t)uni(Sp->t);
       const int nm = min(d, (int)__builtin_ctz(~(unsigned)j));
       for (int l = 0; l < nm; ++l) {
         const int blk = (j >> (l + 1)) >> 6;
@@ -1140,7 +1243,6 @@ struct Chain {
       if (lane == WAVE - 1 && j == (1 << d) - 1)
         Sp->u_top = uniform(key, t, TAG_TOP, (uint32_t)d, 0u);
     }
-    return A_YIELD;
   }
 
   // a gradient arrived for CUR_Q: complete lp / grad, store them, dispatch
@@ -1158,6 +1260,7 @@ struct Chain {
       st(V_CUR_G, g);
       Sp->cur_lp = lp;
       Sp->cur_s2 = s0;
+      if (spec) return leaf_spec(q, p, g, minv, lp, s0);
       return leaf(q, p, g, minv, lp, s0);
     }
     const double lp = finish_grad(g, s0);
@@ -1423,15 +1526,85 @@ struct Chain {
   // dispatch between them).
   __device__ int leaf(const V& q, V p, const V& g, const V& minv, const double cur_lp,
                       const double cur_s2) {
+    const double e = Sp->lf_e;
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) p.a[s] = fma(0.5 * e, g.a[s], p.a[s]);   // end_update_p
+    switch (leaf_book(q, p, g, minv, cur_lp, cur_s2)) {
+      case LB_MID: return leapfrog_stage(q, p, g, minv, e);   // act_leapfrog + act_write_mp
+      case LB_NEXT: return A_BEGIN_SUBTREE;
+      default: return A_END_TREE;
+    }
+  }
+
+  // Speculative leaf (tiles hosting one chain, with a helper wave): the next leaf's
+  // position depends only on this leaf's (q, p, g) -- or, after the last leaf of a
+  // subtree, on the trajectory end the next subtree grows from, whose direction is a
+  // pre-addressed uniform -- not on the merges and U-turn checks.  So the next position
+  // is staged and handed to the gradient waves first; the helper wave computes its prior
+  // part while this wave does the bookkeeping of leaf j.  If the bookkeeping ends the
+  // trajectory, the speculated sweep is drained and discarded.  Same arithmetic on the
+  // same values as the plain path: draws are bitwise identical.
+  __device__ int leaf_spec(const V& q, const V& p, const V& g, const V& minv, const double cur_lp,
+                           const double cur_s2) {
+    const double e = Sp->lf_e;
+    const int d = uni(Sp->depth), j = uni(Sp->leaf);
+    const bool last = j == (1 << d) - 1;
+    if (last && d + 1 >= Pr().max_depth) return leaf(q, p, g, minv, cur_lp, cur_s2);
+    V pe;
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) pe.a[s] = fma(0.5 * e, g.a[s], p.a[s]);   // end_update_p
+    const int dir = uni(Sp->dir);
+    int dirn = dir, dn = d, jn = j + 1;
+    double en = e;
+    V qs = q, ps = pe, gs = g;
+    const uint32_t t = (uint32_t)uni(Sp->t);
+    if (last) {   // act_begin_subtree of depth d + 1
+      dn = d + 1;
+      jn = 0;
+      dirn = (uniform(key, t, TAG_DIR, (uint32_t)dn, 0u) > 0.5) ? 1 : 0;
+      if (dirn != dir) {
+        const int eq = dirn ? V_E1_Q : V_E0_Q;
+        qs = ld(eq);
+        ps = ld(eq + 1);
+        gs = ld(eq + 2);
+      }
+      en = dirn ? Sp->eps_used : -Sp->eps_used;
+    }
+    leapfrog_stage(qs, ps, gs, minv, en);
+    k_q = q; k_pe = pe; k_g = g; k_minv = minv; k_ps = ps; k_gs = gs;
+    k_lp = cur_lp; k_s2 = cur_s2; k_en = en;
+    k_dirn = dirn; k_dn = dn; k_jn = jn; k_t = t;
+    return A_SPEC_STAGED;   // the kernel enqueues the position and posts the helper
+  }
+  // the bookkeeping of the speculated leaf, while its successor is being swept
+  __device__ int act_spec_book() {
+    FITOCT_MARK(act_spec_book);
+    const int r = leaf_book(k_q, k_pe, k_g, k_minv, k_lp, k_s2);
+    if (r == LB_NEXT) {   // the rest of act_begin_subtree (the top merge set depth d + 1)
+      Sp->dir = k_dirn;
+      st(V_PNEAR, k_ps);
+      st(V_CUR_G, k_gs);
+      Sp->cur_lp = Sp->end_lp[k_dirn];
+      Sp->cur_s2 = Sp->end_s2[k_dirn];
+      Sp->leaf = 0;
+      if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;
+      Sp->lf_e = k_en;
+    }
+    return r == LB_END ? A_SPEC_DISCARD : A_SPEC_WAIT;
+  }
+
+  // one leaf of base_nuts::build_tree with the momentum already end-updated: weight,
+  // divergence, every merge it completes and, when the subtree of depth d is complete,
+  // the top-level merge of the transition.  Returns LB_MID (leaf j + 1 of this subtree
+  // is next), LB_NEXT (a subtree of depth d + 1 is next) or LB_END.
+  __device__ int leaf_book(const V& q, const V& p, const V& g, const V& minv, const double cur_lp,
+                           const double cur_s2) {
     FITOCT_MARK(act_leaf);
     long long ts = stamp0();
-    const double e = Sp->lf_e, H0 = Sp->H0;
+    const double H0 = Sp->H0;
     const double sum_metro0 = Sp->sum_metro;
     const int d = uni(Sp->depth), j = uni(Sp->leaf), nlf = uni(Sp->n_leapfrog);
     unsigned used = (unsigned)uni(Sp->pool_used);
-#pragma unroll
-    for (int s = 0; s < PPL; ++s) p.a[s] = fma(0.5 * e, g.a[s], p.a[s]);   // end_update_p
-    st(V_CUR_P, p);
     Sp->n_leapfrog = nlf + 1;
     double h = -cur_lp + kin(p, minv);
     if (isnan(h)) h = INFINITY;
@@ -1442,7 +1615,7 @@ struct Chain {
     sub(1, ts);
     if (h - H0 > 1000.0) {   // divergent: the transition ends here
       Sp->divergent = 1;
-      return A_END_TREE;
+      return LB_END;
     }
 
     V Tpb = p, Trho = p;
@@ -1485,14 +1658,14 @@ struct Chain {
       Tw = Sw;
       if (!okc) {
         Sp->pool_used = (int)used;
-        return A_END_TREE;
+        return LB_END;
       }
     }
     sub(2, ts);
     if (j != (1 << d) - 1) {
       Sp->pool_used = (int)used;
       Sp->leaf = j + 1;
-      return leapfrog_stage(q, p, g, minv, e);   // act_leapfrog + act_write_mp
+      return LB_MID;
     }
     // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
     const int dir = uni(Sp->dir);
@@ -1547,8 +1720,8 @@ struct Chain {
     const bool persist = crit3(far, p, rtot, far, Tpb, rx, near, p, ry, minv);
     st(V_RHO, rtot);
     sub(3, ts);
-    if (!persist || d + 1 >= Pr().max_depth) return A_END_TREE;
-    return A_BEGIN_SUBTREE;
+    if (!persist || d + 1 >= Pr().max_depth) return LB_END;
+    return LB_NEXT;
   }
 
   __device__ void write_draw(double accept, double energy) const {
@@ -1752,7 +1925,7 @@ struct Chain {
   }
 
   // run actions until the chain yields a position to the gradient waves (or finishes)
-  __device__ void run(int a) {
+  __device__ int run(int a) {
     for (;;) {
       FITOCT_MARK(dispatch);
       a = uni(a);
@@ -1765,7 +1938,7 @@ struct Chain {
         pp = (KPc*)(((uint64_t)hi << 32) | lo);
       }
       asm volatile("" : "+s"(a), "+s"(pp));
-      if (a == A_YIELD) break;
+      if (a == A_YIELD || a == A_SPEC_STAGED || a == A_SPEC_WAIT || a == A_SPEC_DISCARD) break;
       const bool prof = kProfile && Pr().stamps != nullptr;
       const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
       const int a0 = a;
@@ -1786,15 +1959,18 @@ struct Chain {
         case A_LEAPFROG: a = act_leapfrog(); break;
         case A_WRITE_MP: a = act_write_mp(); break;
         case A_PRIOR: a = act_prior(); break;
+        case A_SPEC_BOOK: a = act_spec_book(); break;
         default: a = A_YIELD; break;
       }
       if (prof) {
         wave_fence();
-        Sp->prof[0][a0] += (long long)__builtin_amdgcn_s_memtime() - t0;
-        Sp->prof[1][a0] += 1;
+        const int ai = (a0 == A_SPEC_BOOK) ? A_LEAF : a0;   // slot 11: the leaf's bookkeeping
+        Sp->prof[0][ai] += (long long)__builtin_amdgcn_s_memtime() - t0;
+        Sp->prof[1][ai] += 1;
       }
     }
     wave_fence();
+    return a;
   }
 };
 
@@ -1884,7 +2060,7 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane) {
 // parameter blocks, one per problem, and tile_map[2*tile] = {problem, first
 // chain} places each tile; a tile never mixes problems, so every tile still
 // keeps one problem's bins in registers.  tile_map == nullptr: one problem.
-template <class R, int BPT, int NNP, int PPL, int MODE, int FAM, bool MIG>
+template <class R, int BPT, int NNP, int PPL, int MODE, int FAM, bool MIG, bool SPEC>
 __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict__ Pg,
                                                       const int* __restrict__ tile_map) {
   int pidx = 0, c0;
@@ -1905,11 +2081,18 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   __shared__ int q_reserve, n_active, grad_cnt[GMAX];
   __shared__ long long done_t[GMAX];   // profiling build: when the 8th wave finished chain c
   __shared__ long long start_min[GMAX], start_max[GMAX];
+  // speculative leaves (P.spec, one chain per tile): the chain's NUTS wave posts a
+  // request {depth, leaf, iteration} for the prior part of a speculated position; the
+  // helper wave (slot 1) runs it and publishes the request number it finished
+  __shared__ int help_req, help_done, help_arg[3];
+  const bool spec = SPEC && !MIG && nct == 1;
 
   load_kinv<PPL, NNP>(P, L, tid);
   if (tid == 0) {
     q_reserve = 0;
     n_active = nct;
+    help_req = 0;
+    help_done = 0;
   }
   if (tid < GMAX) {
     grad_cnt[tid] = 0;
@@ -2002,8 +2185,30 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     }
     const int c = wave - NGW;
     const bool mig = MIG && P.mig != nullptr;
+    if (spec && c == 1) {   // the helper wave of slot 0's chain
+      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
+      Ch ch(P, L, 0, c0, lane, nct);
+      int seen = 0;
+      long long spins = 0;
+      for (;;) {
+        const int r = lds_load(&help_req);
+        if (r < 0) break;                       // the chain has finished
+        if (r == seen) {
+          if (++spins > SPIN_LIMIT) break;
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        spins = 0;
+        seen = r;
+        wave_fence();   // the request's arguments are read after its number
+        ch.prior_and_uniforms(true, lds_load(&help_arg[0]), lds_load(&help_arg[1]),
+                              (uint32_t)lds_load(&help_arg[2]));
+        wave_fence();
+        if (lane == 0) __atomic_store_n(&help_done, seen, __ATOMIC_RELAXED);
+      }
+    }
     if (c < (mig ? P.G : nct)) {
-      using Ch = Chain<PPL, NNP, FAM, MIG>;
+      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
       long long epoch = 0;     // this slot's hand-offs (grad_cnt[c] counts NGW per epoch)
       int lc = c < nct ? c0 + c : -1;
       int a = Ch::A_INIT_STATE;
@@ -2013,10 +2218,61 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         long long steps = 0;
         bool in_sweep = false;   // the last run() was A_PRIOR, overlapping the chain's sweep
         // ONE call site of the action machine (it is inlined once, not per caller)
+        int hreq = 0;            // helper requests posted (speculative path)
         for (;;) {
           FITOCT_MARK(nuts_loop);
         const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
-        ch.run(a);
+        const int y = ch.run(a);
+        if (spec && y == Ch::A_SPEC_STAGED) {   // enqueue the speculated position, hand its prior part over
+          if (++steps > P.max_steps) {
+            ch.Sp->status = ERR_TIMEOUT;
+            a = Ch::A_FINISH;
+            continue;
+          }
+          if (lane == 0) {
+            const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
+            __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
+                             __ATOMIC_RELAXED);
+            help_arg[0] = ch.k_dn;
+            help_arg[1] = ch.k_jn;
+            help_arg[2] = (int)ch.k_t;
+            wave_fence();   // the arguments land before the request number
+            __atomic_store_n(&help_req, hreq + 1, __ATOMIC_RELAXED);
+          }
+          if (stamp) t_enq = (long long)__builtin_amdgcn_s_memtime();
+          ++hreq;
+          ++epoch;
+          a = Ch::A_SPEC_BOOK;
+          continue;
+        }
+        if (spec && (y == Ch::A_SPEC_WAIT || y == Ch::A_SPEC_DISCARD)) {
+          long long spins = 0;
+          const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+          if (stamp) t_busy += w0 - s0;
+          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch) || lds_load(&help_done) < hreq) {
+            if (++spins > SPIN_LIMIT) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          wave_fence();   // nothing of the next action is read before the sweep and the helper are done
+          if (stamp) {
+            const long long t1 = (long long)__builtin_amdgcn_s_memtime();
+            t_wait += t1 - w0;
+            t_sweep += done_t[c] - t_enq;
+            t_st0 += start_min[c] - t_enq;
+            t_st1 += start_max[c] - t_enq;
+            start_min[c] = 0x7FFFFFFFFFFFFFFFLL;
+            start_max[c] = 0;
+            t_notice += t1 - (done_t[c] > w0 ? done_t[c] : w0);
+            ++n_items;
+          }
+          if (spins > SPIN_LIMIT) {
+            ch.Sp->status = ERR_TIMEOUT;
+            a = Ch::A_FINISH;
+          } else {
+            a = (y == Ch::A_SPEC_WAIT) ? Ch::A_GRAD : Ch::A_END_TREE;
+          }
+          continue;
+        }
         if (in_sweep) {
           in_sweep = false;
           long long spins = 0;
@@ -2061,7 +2317,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           ++n_items;
         }
         const int stt = __builtin_amdgcn_readfirstlane(ch.Sp->state);
-        if (stt == ST_DONE || stt == ST_MOVED) break;
+        if (stt == ST_DONE || stt == ST_MOVED) {
+          if (spec && lane == 0) __atomic_store_n(&help_req, -1, __ATOMIC_RELAXED);   // release the helper
+          break;
+        }
         if (++steps > P.max_steps) {   // termination guarantee: report, never hang
           ch.Sp->status = ERR_TIMEOUT;
           a = Ch::A_FINISH;
@@ -2218,8 +2477,10 @@ static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int t
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP);
   } else {
-    auto k = P.mig != nullptr ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, true>
-                              : nuts_kernel<R, BPT, NNP, PPL, MODE, F, false>;
+    // three samplers: with migration, with speculative leaves (one chain per tile), plain
+    auto k = P.mig != nullptr ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, true, false>
+             : P.spec ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, false, true>
+                      : nuts_kernel<R, BPT, NNP, PPL, MODE, F, false, false>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP, tile_map);
   }

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FITOCT_ABI_VERSION 1
+#define FITOCT_ABI_VERSION 2
 /* largest accepted N (depth bins): bounds every host and device allocation derived from it */
 #define FITOCT_MAX_BINS (1 << 22)
 
@@ -136,7 +136,18 @@ typedef struct fitoct_plan_info {
   int32_t lds_bytes;
   int32_t n_pad;           /* padded bin count */
   int64_t draws_bytes;     /* size of the draws buffer */
+  int32_t sampler;         /* sampler variant launched: FITOCT_SAMPLER_* */
+  int32_t reserved;
 } fitoct_plan_info;
+
+/* fitoct_plan_info::sampler.  PLAIN: tiles of several chains, or migration off;
+ * MIGRATE: chains move between tiles at transition boundaries (work balance);
+ * SPECULATIVE: one chain per tile, whose next leapfrog position is swept while the
+ * current leaf's tree bookkeeping runs (FITOCT_NO_SPEC=1 turns it off).  The draws
+ * are the same bit for bit whichever variant runs. */
+#define FITOCT_SAMPLER_PLAIN 0
+#define FITOCT_SAMPLER_MIGRATE 1
+#define FITOCT_SAMPLER_SPECULATIVE 2
 
 typedef struct fitoct_plan fitoct_plan;
 

@@ -1,7 +1,8 @@
 """Bitwise A/B of variant libraries: every abtest/lib_*.so samples the same short
 runs (configs 2, 3, 4 shapes and a batch of config-5 files), and each variant's draws
 are compared bit for bit (SHA-256 of the draw arrays) with abtest/lib_base.so.  Latency-only changes (same
-arithmetic) must print 'identical'.
+arithmetic) must print 'identical'.  abtest/env_<name> (KEY=VALUE lines), when present, is added to
+lib_<name>'s environment (e.g. a copy of a library run with a switch set).
 
     python scripts/ab_bitwise.py            # on the GPU box
 """
@@ -48,6 +49,9 @@ def main():
     for lib in libs:
         name = os.path.basename(lib)[4:-3]
         env = dict(os.environ, FITOCT_LIB_PATH=lib)
+        envf = os.path.join(ROOT, "abtest", "env_" + name)
+        if os.path.exists(envf):
+            env.update(line.strip().split("=", 1) for line in open(envf) if "=" in line)
         r = subprocess.run([sys.executable, "-c", RUNNER % ROOT, os.path.join(OUT, name + ".json")],
                            env=env, timeout=300)
         if r.returncode != 0:
