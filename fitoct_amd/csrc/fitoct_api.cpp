@@ -8,6 +8,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <climits>
 #include <chrono>
 #include <memory>
 #include <string>
@@ -917,6 +918,39 @@ int32_t fitoct_plan_wait(fitoct_plan* pl) {
               tno / std::max(nw, 1.0));
       fprintf(stderr, "[fitoct stamps] enqueue -> first wave starts %.0f, last wave starts %.0f\n",
               ts0 / std::max(nw, 1.0), ts1 / std::max(nw, 1.0));
+      // tile timeline on the 100 MHz clock: how much of the launch the tiles sit idle at
+      // the end (the kernel ends with its last tile)
+      {
+        long long t0 = LLONG_MAX, t1 = 0;
+        std::vector<double> ends, firsts;
+        for (int t = 0; t < pl->tiles; ++t) {
+          const long long* o = h.data() + (size_t)NSTAMP * t;
+          t0 = std::min(t0, o[64]);
+          t1 = std::max(t1, o[65]);
+        }
+        const double span = std::max(1.0, (double)(t1 - t0));
+        double done_sum = 0;
+        for (int t = 0; t < pl->tiles; ++t) {
+          const long long* o = h.data() + (size_t)NSTAMP * t;
+          ends.push_back((o[65] - t0) / span);
+          if (o[66] > 0) firsts.push_back((o[66] - t0) / span);
+          done_sum += o[67];
+        }
+        std::sort(ends.begin(), ends.end());
+        std::sort(firsts.begin(), firsts.end());
+        auto q = [](const std::vector<double>& v, double f) {
+          return v.empty() ? 0.0 : v[std::min(v.size() - 1, (size_t)(f * (v.size() - 1)))];
+        };
+        double mean_end = 0;
+        for (double e : ends) mean_end += e;
+        mean_end /= std::max<size_t>(1, ends.size());
+        fprintf(stderr,
+                "[fitoct stamps] tile ends (fraction of the launch): mean %.3f p10 %.3f p50 %.3f "
+                "p90 %.3f | first chain done in a tile: p10 %.3f p50 %.3f p90 %.3f | chains "
+                "finished %.0f, launch %.1f ms\n",
+                mean_end, q(ends, 0.1), q(ends, 0.5), q(ends, 0.9), q(firsts, 0.1), q(firsts, 0.5),
+                q(firsts, 0.9), done_sum, span / 1e5);
+      }
     }
     pl->ran = true;
     return FITOCT_OK;

@@ -64,11 +64,10 @@ namespace fitoct {
 using KPc = const AS_CST KParams;
 
 enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2, FAM_MONO = 3 };
-#ifndef FITOCT_EXP11
-#define FITOCT_EXP11 0
-#endif
-#ifndef FITOCT_RCP2
-#define FITOCT_RCP2 0
+// FITOCT_PAIRED_BINS=0 builds the 8-bins-per-lane sweep with one reciprocal per bin and
+// Taylor-12 exp, as the other widths (A/B of bin_poly_fwd2)
+#ifndef FITOCT_PAIRED_BINS
+#define FITOCT_PAIRED_BINS 1
 #endif
 
 // Cycle stamps (FITOCT_STAMPS) exist only in a profiling build
@@ -373,7 +372,31 @@ template <> __device__ __forceinline__ double exp_<double>(double x) {
   const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
   double r = fma(-n, 6.93147180369123816490e-01, x);
   r = fma(-n, 1.90821492927058770002e-10, r);
-#if FITOCT_EXP11
+  double p = 2.08767569878680989792e-09;   // 1/12!
+  p = fma(p, r, 2.50521083854417187751e-08);
+  p = fma(p, r, 2.75573192239858906526e-07);
+  p = fma(p, r, 2.75573192239858906526e-06);
+  p = fma(p, r, 2.48015873015873015873e-05);
+  p = fma(p, r, 1.98412698412698412698e-04);
+  p = fma(p, r, 1.38888888888888888889e-03);
+  p = fma(p, r, 8.33333333333333333333e-03);
+  p = fma(p, r, 4.16666666666666666667e-02);
+  p = fma(p, r, 1.66666666666666666667e-01);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, ni);
+}
+template <> __device__ __forceinline__ float exp_<float>(float x) { return __expf(x); }
+// exp_ with a degree-11 polynomial: same reduction, one FMA fewer
+__device__ __forceinline__ double exp11_(double x) {
+  x = fmax(x, -746.0);
+  const double SH = 6755399441055744.0;
+  const double t = fma(x, 1.4426950408889634, SH);
+  const double n = t - SH;
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
+  double r = fma(-n, 6.93147180369123816490e-01, x);
+  r = fma(-n, 1.90821492927058770002e-10, r);
   // degree-11 Chebyshev fit on |r| <= ln2/2 (scripts/micro/exp_fit.py): <= 1 ulp from the
   // correctly rounded exp, one FMA fewer than Taylor-12
   double p = 2.5110037605963777e-08;
@@ -388,24 +411,8 @@ template <> __device__ __forceinline__ double exp_<double>(double x) {
   p = fma(p, r, 0.5000000000000019);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
-#else
-  double p = 2.08767569878680989792e-09;   // 1/12!
-  p = fma(p, r, 2.50521083854417187751e-08);
-  p = fma(p, r, 2.75573192239858906526e-07);
-  p = fma(p, r, 2.75573192239858906526e-06);
-  p = fma(p, r, 2.48015873015873015873e-05);
-  p = fma(p, r, 1.98412698412698412698e-04);
-  p = fma(p, r, 1.38888888888888888889e-03);
-  p = fma(p, r, 8.33333333333333333333e-03);
-  p = fma(p, r, 4.16666666666666666667e-02);
-  p = fma(p, r, 1.66666666666666666667e-01);
-  p = fma(p, r, 0.5);
-  p = fma(p, r, 1.0);
-  p = fma(p, r, 1.0);
-#endif
   return ldexp(p, ni);
 }
-template <> __device__ __forceinline__ float exp_<float>(float x) { return __expf(x); }
 
 // Likelihood terms of one bin given its modulation dL (shared by every mode).
 // acc: [0] sum d^2, [1] sum a, [2] sum a e, [3] sum w; returns h (adjoint seed of dL).
@@ -413,7 +420,9 @@ template <> __device__ __forceinline__ float exp_<float>(float x) { return __exp
 // (umin), applied once after the lane's bins (no per-bin selects).
 template <class R, class A, int NA>
 __device__ __forceinline__ R bin_tail(R iL, R cx, R y, R isu, R th1, R th2, A (&acc)[NA]) {
-  const R e = exp_<R>(-cx * iL);                                 // exp(-c x / L)
+  R e;                                                           // exp(-c x / L)
+  if constexpr (sizeof(R) == 8) e = exp11_(-cx * iL);
+  else e = exp_<R>(-cx * iL);
   const R m = fma(th2, e, th1);                                  // ui.R:88
   const R d = (y - m) * isu;                                     // (y-m)/uy
   const R a = d * isu;                                           // dlp/dm * sigma^2
@@ -710,17 +719,6 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         double w[8];
-#if FITOCT_RCP2
-#pragma unroll
-        for (int b = 0; b < 8; b += 2) {
-          const int bb = half * 8 + b;
-          bin_poly_fwd2<R, NNP, double>(
-              cx0 + P.geo_dcx[bb], bins.y[bb], bins.isu[bb], fmin(t0 * P.geo_R[bb], tmax),
-              bins.row[bb][1], cx0 + P.geo_dcx[bb + 1], bins.y[bb + 1], bins.isu[bb + 1],
-              fmin(t0 * P.geo_R[bb + 1], tmax), bins.row[bb + 1][1], th1, th2, th3, cf, acc, umin,
-              w[b], w[b + 1]);
-        }
-#else
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
           const int bb = half * 8 + b;
@@ -729,23 +727,22 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
           w[b] = bin_poly_fwd<R, NNP, double>(cxb, bins.y[bb], bins.isu[bb], tb,
                                               bins.row[bb][1], th1, th2, th3, cf, acc, umin);
         }
-#endif
         moments_geo_add<8, NNP>(P, half ? t0 * P.geo_R[8] : t0, w, acc);
       }
     } else if constexpr (BPT > 0 && MODE == MODE_POLY && sizeof(R) == 8) {
       if (P.geo) {
         double w[BPT];
-#if FITOCT_RCP2
-        if constexpr (BPT % 2 == 0) {
+        // 8 bins per lane (the headline shape, N = 2048): bins in pairs sharing one
+        // reciprocal, exp by a degree-11 polynomial (A/B: config 3 +1.7 %, configs 2 / 5
+        // within noise; at 16 bins the pairs spill)
+        if constexpr (BPT == 8 && FITOCT_PAIRED_BINS) {
 #pragma unroll
           for (int b = 0; b < BPT; b += 2)
             bin_poly_fwd2<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
                                           bins.row[b][1], bins.cx[b + 1], bins.y[b + 1],
                                           bins.isu[b + 1], bins.row[b + 1][0], bins.row[b + 1][1],
                                           th1, th2, th3, cf, acc, umin, w[b], w[b + 1]);
-        } else
-#endif
-        {
+        } else {
 #pragma unroll
           for (int b = 0; b < BPT; ++b)
             w[b] = bin_poly_fwd<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
@@ -2118,6 +2115,15 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   long long t_busy = 0, n_items = 0, t_wait = 0, t_enq = 0, t_sweep = 0, t_notice = 0;
   long long t_st0 = 0, t_st1 = 0;
   long long t_begin = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  // tile timeline (profiling build): start, first chain finished, end, on the 100 MHz clock
+  __shared__ long long first_done_rt;
+  __shared__ int chains_done_here;
+  const long long rt_begin = kProfile ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+  if (kProfile && tid == 0) {
+    first_done_rt = 0;
+    chains_done_here = 0;
+  }
+  if (kProfile) __syncthreads();
   if (wave < NGW) {  // ------------------------- gradient waves
     Bins<R, BPT, NNP, MODE> bins;
     bins.load(P, tid);
@@ -2318,6 +2324,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         }
         const int stt = __builtin_amdgcn_readfirstlane(ch.Sp->state);
         if (stt == ST_DONE || stt == ST_MOVED) {
+          if (kProfile && lane == 0 && stt == ST_DONE) {
+            atomicCAS((unsigned long long*)&first_done_rt, 0ULL,
+                      (unsigned long long)__builtin_amdgcn_s_memrealtime());
+            atomicAdd(&chains_done_here, 1);
+          }
           if (spec && lane == 0) __atomic_store_n(&help_req, -1, __ATOMIC_RELAXED);   // release the helper
           break;
         }
@@ -2376,6 +2387,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       o[0] = n_items;
       o[1] = t_busy;
       o[3] = (long long)__builtin_amdgcn_s_memtime() - t_begin;
+      o[64] = rt_begin;
+      o[65] = (long long)__builtin_amdgcn_s_memrealtime();
+      o[66] = first_done_rt;
+      o[67] = chains_done_here;
     } else {
       o[2] = t_busy;
       o[40] = t_wait;

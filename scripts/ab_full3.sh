@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B at full length on the headline workload (config 3, 500 + 1000 iterations): effects
+# on the launch's tail (load balance) do not show in the short runs of ab_libs.sh.
+cd "$GRAFT_REPO_ROOT"
+for rep in 1 2; do
+  for l in abtest/lib_*.so; do
+    n=$(basename $l .so); n=${n#lib_}
+    envs=""; [ -f abtest/env_$n ] && envs=$(cat abtest/env_$n)
+    env $envs FITOCT_LIB_PATH=$PWD/$l timeout -k 10 200 python3 bench.py --config 3 --steps 1 --warmup 0 --no-cpu 2>>gpurun_out/ab_stderr.log | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print('$l config 3 full', d['value'], d['roofline']['kernel_ms'], 'TF', d['roofline']['achieved'])" || exit 1
+  done
+done
