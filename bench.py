@@ -49,7 +49,7 @@ CONFIGS = {
 }
 FP64_VALU_PEAK_TF = 78.6          # MI355X FP64 vector peak (vendor spec; 1/2 of FP32 vector)
 HBM_PEAK_GBS = 8000.0
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
 def f_grad(N, Nn):
