@@ -197,8 +197,12 @@ def _single_hip_runtime():
         pass
 
 
+ABI_VERSION = 2   # include/fitoct.h FITOCT_ABI_VERSION
+
+
 def lib():
-    """Load the in-tree libfitoct.so (fails loudly if it was not built)."""
+    """Load the in-tree libfitoct.so (fails loudly if it was not built or is not the
+    ABI this binding was written for)."""
     global _LIB
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
@@ -211,6 +215,15 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        # the binding's structs must be the library's
+        if L.fitoct_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH}: ABI {L.fitoct_abi_version()}, this binding needs "
+                              f"{ABI_VERSION} (rebuild with `python -m fitoct_amd.build`)")
+        sz = [C.c_int32() for _ in range(4)]
+        L.fitoct_struct_sizes(*[C.byref(v) for v in sz])
+        want = (C.sizeof(Problem), C.sizeof(Config), C.sizeof(Result), C.sizeof(PlanInfo))
+        if tuple(v.value for v in sz) != want:
+            raise ImportError(f"{LIB_PATH}: struct sizes {tuple(v.value for v in sz)} != binding {want}")
         _LIB = L
     return _LIB
 

@@ -96,6 +96,7 @@ enum VecId : int {
   V_RHO, V_PNEAR,              // trajectory momentum sum, near end of old trajectory
   V_QS, V_QE,                  // staged q and its constrained values (exp on positive params)
   V_PG, V_CA,                  // prior part of grad, likelihood coefficient (prior_part)
+  V_SPEC_PE,                   // speculative path: the booked leaf's end-updated momentum
   NVEC
 };
 // U-turn record of one tree level (LDS)
@@ -107,12 +108,13 @@ constexpr int NAUX = 96;   // per chain: yGP[32] | horseshoe lambda_j*tau [32] |
 struct ChainScalars {
   int state, t, depth, leaf, dir, n_leapfrog, divergent, init_attempt;
   int da_counter, win_counter, win_size, win_next, wf_n, ss_trial, ss_dir, ss_window;
-  int status, win_on, init_buf, term_buf, pool_used, lsw_e, pad1, pad2;
+  int status, win_on, init_buf, term_buf, pool_used, lsw_e, spec_we, pad2;
   int st_prop[MAXDEPTH];
   int st_w_e[MAXDEPTH];
   double H0, lsw_m, sum_metro, eps, eps_used, mu, s_bar, x_bar, ss_H0, lf_e;
   double cur_lp, cur_s2, smp_lp, smp_s2;
-  double pr_lp, pr_is2, u_top, pad4;
+  double pr_lp, pr_is2, u_top, spec_lp;
+  double spec_h, spec_wl, spec_wm, pad5;   // speculative path: the booked leaf's energy and weight
   int u_blk[MAXDEPTH];     // which block of 64 merge uniforms each level's ring holds (-1: none)
   double end_lp[2], end_s2[2];
   double st_w_m[MAXDEPTH];
@@ -122,6 +124,8 @@ struct ChainScalars {
   long long prof[2][32];   // diagnostic build: cycles and calls per action
 };
 static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
+
+constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded, never hang a box
 
 __device__ __forceinline__ void wave_fence() {
   // orders this wave's LDS traffic: every earlier ds_* op has completed and the
@@ -835,6 +839,9 @@ struct Chain {
   double k_lp, k_s2, k_en;
   int k_dirn, k_dn, k_jn;
   uint32_t k_t;
+  // the helper publishes the booked leaf's weight by writing request numbers here
+  volatile AS_LDS int* help_wdone = nullptr;
+  int help_want = 0;
   RngKey key;
 
   __device__ Chain(KPc& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
@@ -1568,6 +1575,8 @@ struct Chain {
       en = dirn ? Sp->eps_used : -Sp->eps_used;
     }
     leapfrog_stage(qs, ps, gs, minv, en);
+    st(V_SPEC_PE, pe);   // for the helper: this leaf's energy and weight (spec_weight)
+    Sp->spec_lp = cur_lp;
     k_q = q; k_pe = pe; k_g = g; k_minv = minv; k_ps = ps; k_gs = gs;
     k_lp = cur_lp; k_s2 = cur_s2; k_en = en;
     k_dirn = dirn; k_dn = dn; k_jn = jn; k_t = t;
@@ -1576,7 +1585,7 @@ struct Chain {
   // the bookkeeping of the speculated leaf, while its successor is being swept
   __device__ int act_spec_book() {
     FITOCT_MARK(act_spec_book);
-    const int r = leaf_book(k_q, k_pe, k_g, k_minv, k_lp, k_s2);
+    const int r = leaf_book_split(k_q, k_pe, k_g, k_minv, k_lp, k_s2);
     if (r == LB_NEXT) {   // the rest of act_begin_subtree (the top merge set depth d + 1)
       Sp->dir = k_dirn;
       st(V_PNEAR, k_ps);
@@ -1588,6 +1597,175 @@ struct Chain {
       Sp->lf_e = k_en;
     }
     return r == LB_END ? A_SPEC_DISCARD : A_SPEC_WAIT;
+  }
+
+  // run by the helper wave for the leaf being booked: its Hamiltonian and multinomial
+  // weight, the same operations as leaf_book's first lines
+  __device__ void spec_weight() const {
+    const V pe = ld(V_SPEC_PE), minv = ld(V_MINV);
+    double h = -Sp->spec_lp + kin(pe, minv);
+    if (isnan(h)) h = INFINITY;
+    const double wl = Sp->H0 - h;
+    const XF w = xf_exp(wl);
+    Sp->spec_h = h;
+    Sp->spec_wl = wl;
+    Sp->spec_wm = w.m;
+    Sp->spec_we = w.e;
+  }
+
+  // leaf_book for the speculative path, split so that the weight can come from the
+  // helper wave: first every U-turn check the leaf completes (they need momenta only:
+  // the running subtree's begin momentum and momentum sum follow the levels'
+  // records whatever the multinomial choices), including the trajectory-level check
+  // when the subtree ends; then, with the helper's weight, the divergence test, the
+  // multinomial merges up to the first failing check, the push and the top-level
+  // merge.  Same operations on the same values as leaf_book, so the same outcome.
+  __device__ int leaf_book_split(const V& q, const V& p, const V& g, const V& minv,
+                                 const double cur_lp, const double cur_s2) {
+    FITOCT_MARK(act_leaf_split);
+    long long ts = stamp0();
+    const double H0 = Sp->H0;
+    const double sum_metro0 = Sp->sum_metro;
+    const int d = uni(Sp->depth), j = uni(Sp->leaf), nlf = uni(Sp->n_leapfrog);
+    unsigned used = (unsigned)uni(Sp->pool_used);
+    Sp->n_leapfrog = nlf + 1;
+    const int nm = min(d, (int)__builtin_ctz(~(unsigned)j));   // merges this leaf completes
+    const bool last = j == (1 << d) - 1;
+    // phase A: U-turn checks
+    V Tpb = p, Trho = p;
+    int fail = nm;
+#pragma unroll 1
+    for (int l = 0; l < nm; ++l) {
+      const V Ipb = lld(l, K_PBEG), Ipe = lld(l, K_PEND), Irho = lld(l, K_RHO);
+      V rsub, rx, ry;
+#pragma unroll
+      for (int s = 0; s < PPL; ++s) {
+        rsub.a[s] = Irho.a[s] + Trho.a[s];
+        rx.a[s] = Irho.a[s] + Tpb.a[s];
+        ry.a[s] = Trho.a[s] + Ipe.a[s];
+      }
+      const bool okc = crit3(Ipb, p, rsub, Ipb, Tpb, rx, Ipe, p, ry, minv);
+      Tpb = Ipb;
+      Trho = rsub;
+      if (!okc) {
+        fail = l;
+        break;
+      }
+    }
+    const int dir = uni(Sp->dir);
+    V rtot;
+    bool persist = false;
+    if (last && fail == nm) {
+      const V far = ld(dir ? V_E0_P : V_E1_P), near = ld(V_PNEAR), rho = ld(V_RHO);
+      V rx, ry;
+#pragma unroll
+      for (int s = 0; s < PPL; ++s) {
+        rtot.a[s] = rho.a[s] + Trho.a[s];
+        rx.a[s] = rho.a[s] + Tpb.a[s];
+        ry.a[s] = Trho.a[s] + near.a[s];
+      }
+      persist = crit3(far, p, rtot, far, Tpb, rx, near, p, ry, minv);
+    }
+    sub(2, ts);
+    // phase B: the helper's weight of this leaf
+    long long spins = 0;
+    while (*help_wdone < help_want) {
+      if (++spins > SPIN_LIMIT) {
+        Sp->status = ERR_TIMEOUT;
+        return LB_END;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    wave_fence();
+    const double h = Sp->spec_h, wl = Sp->spec_wl;
+    const XF wleaf{Sp->spec_wm, uni(Sp->spec_we)};
+    Sp->sum_metro = sum_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
+    sub(1, ts);
+    if (h - H0 > 1000.0) {   // divergent: the transition ends here
+      Sp->divergent = 1;
+      return LB_END;
+    }
+    XF Tw = wleaf;
+    int Tprop = -1;   // -1: the current leaf (CUR); else a pool slot
+    const int nmerge = fail < nm ? fail + 1 : nm;
+#pragma unroll 1
+    for (int l = 0; l < nmerge; ++l) {
+      const XF Iw{Sp->st_w_m[l], Sp->st_w_e[l]};
+      const double um = RNG[l * WAVE + ((j >> (l + 1)) & (WAVE - 1))];
+      const int Iprop = uni(Sp->st_prop[l]);
+      const XF Sw = xf_add(Iw, Tw);
+      const bool take_final = xf_gt(Tw, Sw) || xf_u_below(um, Tw, Sw);
+      if (take_final) {
+        used &= ~(1u << Iprop);
+      } else {
+        if (Tprop >= 0) used &= ~(1u << Tprop);
+        Tprop = Iprop;
+      }
+      Tw = Sw;
+    }
+    if (fail < nm) {
+      Sp->pool_used = (int)used;
+      return LB_END;
+    }
+    if (nm < d) {   // push the running subtree as the init subtree of level nm + 1
+      lst(nm, K_PBEG, Tpb);
+      lst(nm, K_PEND, p);
+      lst(nm, K_RHO, Trho);
+      Sp->st_w_m[nm] = Tw.m;
+      Sp->st_w_e[nm] = Tw.e;
+      Sp->st_prop[nm] = (Tprop < 0) ? pool_put(used, q, p, g, cur_lp, cur_s2) : Tprop;
+    }
+    sub(0, ts);
+    if (!last) {
+      Sp->pool_used = (int)used;
+      Sp->leaf = j + 1;
+      return LB_MID;
+    }
+    // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
+    const XF Ww{Sp->lsw_m, Sp->lsw_e};
+    const double u_top = Sp->u_top;
+    const int eq = dir ? V_E1_Q : V_E0_Q;
+    st(eq, q);
+    st(eq + 1, p);
+    st(eq + 2, g);
+    Sp->end_lp[dir] = cur_lp;
+    Sp->end_s2[dir] = cur_s2;
+    Sp->depth = d + 1;
+    const bool take = xf_gt(Tw, Ww) || xf_u_below(u_top, Tw, Ww);
+    if (take) {
+      if (Tprop < 0) {
+        st(V_SMP_Q, q);
+        st(V_SMP_P, p);
+        st(V_SMP_G, g);
+        Sp->smp_lp = cur_lp;
+        Sp->smp_s2 = cur_s2;
+      } else {
+        const AS_GLB double* sq = pslot(Tprop, P_Q);
+        const AS_GLB double* sp = pslot(Tprop, P_P);
+        const AS_GLB double* sg = pslot(Tprop, P_G);
+        V q2, p2, g2;
+#pragma unroll
+        for (int s = 0; s < PPL; ++s) {
+          q2.a[s] = sq[idx(s)];
+          p2.a[s] = sp[idx(s)];
+          g2.a[s] = sg[idx(s)];
+        }
+        st(V_SMP_Q, q2);
+        st(V_SMP_P, p2);
+        st(V_SMP_G, g2);
+        Sp->smp_lp = Sp->pool_lp[Tprop];
+        Sp->smp_s2 = Sp->pool_s2[Tprop];
+      }
+    }
+    if (Tprop >= 0) used &= ~(1u << Tprop);
+    Sp->pool_used = (int)used;
+    const XF Wn = xf_add(Ww, Tw);
+    Sp->lsw_m = Wn.m;
+    Sp->lsw_e = Wn.e;
+    st(V_RHO, rtot);
+    sub(3, ts);
+    if (!persist || d + 1 >= Pr().max_depth) return LB_END;
+    return LB_NEXT;
   }
 
   // one leaf of base_nuts::build_tree with the momentum already end-updated: weight,
@@ -2000,7 +2178,6 @@ constexpr int RINGN = 16;                 // hand-off ring: >= 2 * GMAX entries
 #ifndef FITOCT_NUTS_WAIT_PRIO
 #define FITOCT_NUTS_WAIT_PRIO 0
 #endif
-constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded, never hang a box
 
 // Migration receiver: post NUTS slot c of this tile as free and wait until a
 // crowded tile hands a chain over (returns its chain index, image loaded into
@@ -2081,7 +2258,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   // speculative leaves (P.spec, one chain per tile): the chain's NUTS wave posts a
   // request {depth, leaf, iteration} for the prior part of a speculated position; the
   // helper wave (slot 1) runs it and publishes the request number it finished
-  __shared__ int help_req, help_done, help_arg[3];
+  __shared__ int help_req, help_done, help_wdone, help_arg[3];
   const bool spec = SPEC && !MIG && nct == 1;
 
   load_kinv<PPL, NNP>(P, L, tid);
@@ -2090,6 +2267,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     n_active = nct;
     help_req = 0;
     help_done = 0;
+    help_wdone = 0;
   }
   if (tid < GMAX) {
     grad_cnt[tid] = 0;
@@ -2207,6 +2385,9 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         spins = 0;
         seen = r;
         wave_fence();   // the request's arguments are read after its number
+        ch.spec_weight();   // first what the chain's bookkeeping waits for
+        wave_fence();
+        if (lane == 0) __atomic_store_n(&help_wdone, seen, __ATOMIC_RELAXED);
         ch.prior_and_uniforms(true, lds_load(&help_arg[0]), lds_load(&help_arg[1]),
                               (uint32_t)lds_load(&help_arg[2]));
         wave_fence();
@@ -2248,6 +2429,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           if (stamp) t_enq = (long long)__builtin_amdgcn_s_memtime();
           ++hreq;
           ++epoch;
+          ch.help_wdone = (volatile AS_LDS int*)&help_wdone;
+          ch.help_want = hreq;
           a = Ch::A_SPEC_BOOK;
           continue;
         }
