@@ -428,9 +428,7 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   k.G = G;
   k.max_depth = max_depth;
   k.nuts_prio = getenv("FITOCT_NUTS_PRIO") ? atoi(getenv("FITOCT_NUTS_PRIO")) : 3;
-  // one chain per tile leaves three NUTS slots idle: one of them helps the chain's
-  // NUTS wave (speculative leaves, nuts_device.hip leaf_spec); FITOCT_NO_SPEC=1: off
-  k.spec = (G == 1 && getenv("FITOCT_NO_SPEC") == nullptr) ? 1 : 0;
+  k.spec = 0;   // set below, once migration is decided
   pl->tiles = (chains + G - 1) / G;
   pl->lds = lds_bytes(pl->ppl, G, max_depth);
   return FITOCT_OK;
@@ -756,6 +754,16 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
     k.mig_img = pl->d_mig_img;
     k.mig_tiles = T;
     k.mig_img_words = words;
+  }
+  // speculative leaves (nuts_device.hip leaf_spec) in tiles of one chain, where a spare
+  // NUTS wave helps it (config 2 +4 %).  Tiles of several chains have no spare wave and
+  // lose 10 % with it (config 5), so they run the plain sampler unless FITOCT_SPEC=1
+  // (tests; any plan without migration).  FITOCT_NO_SPEC=1: the plain sampler always.
+  {
+    const char* fs = getenv("FITOCT_SPEC");
+    bool on = pl->mig_bytes == 0 && (fs != nullptr ? atoi(fs) != 0 : k.G == 1);
+    if (getenv("FITOCT_NO_SPEC") != nullptr) on = false;
+    k.spec = on ? 1 : 0;
   }
   *out = guard.release();
   return FITOCT_OK;

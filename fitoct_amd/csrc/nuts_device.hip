@@ -114,11 +114,11 @@ struct ChainScalars {
   double H0, lsw_m, sum_metro, eps, eps_used, mu, s_bar, x_bar, ss_H0, lf_e;
   double cur_lp, cur_s2, smp_lp, smp_s2;
   double pr_lp, pr_is2, u_top, spec_lp;
-  double spec_h, spec_wl, spec_wm, pad5;   // speculative path: the booked leaf's energy and weight
   int u_blk[MAXDEPTH];     // which block of 64 merge uniforms each level's ring holds (-1: none)
   double end_lp[2], end_s2[2];
   double st_w_m[MAXDEPTH];
   double pool_lp[MAXDEPTH + 1], pool_s2[MAXDEPTH + 1];
+  double spec_h, spec_wl, spec_wm, pad5;   // speculative path: the booked leaf's energy and weight
   long long leapfrogs;
   long long pad3;
   long long prof[2][32];   // diagnostic build: cycles and calls per action
@@ -833,7 +833,8 @@ struct Chain {
   double krow[KROW ? NNP : 1];
   const AS_LDS double* bv;
   int lane, slot, lc, gid, nct;
-  bool spec;   // speculative leaves with a helper wave (KParams::spec: one chain per tile)
+  static constexpr bool spec = SPEC && !MIG;   // speculative leaves (the SPEC sampler)
+  bool helped;   // ... with a helper wave (tiles of one chain); else this wave does its part
   // a speculated leaf's values, kept from leaf_spec to act_spec_book (across the hand-off)
   V k_q, k_pe, k_g, k_minv, k_ps, k_gs;
   double k_lp, k_s2, k_en;
@@ -850,7 +851,7 @@ struct Chain {
         part(L.part()), Kinv(L.kinv()), bv(L.bv()),
         lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
     gid = Pr().chain_offset + lc;
-    spec = SPEC && !MIG && nct_ == 1;
+    helped = spec && nct_ == 1;
     key = make_key(Pr().seed, (uint32_t)gid);
     if constexpr (KROW) {
       const int r = lane < NNP ? lane : 0;
@@ -1264,7 +1265,7 @@ struct Chain {
       st(V_CUR_G, g);
       Sp->cur_lp = lp;
       Sp->cur_s2 = s0;
-      if (spec) return leaf_spec(q, p, g, minv, lp, s0);
+      if constexpr (spec) return leaf_spec(q, p, g, minv, lp, s0);
       return leaf(q, p, g, minv, lp, s0);
     }
     const double lp = finish_grad(g, s0);
@@ -1585,6 +1586,7 @@ struct Chain {
   // the bookkeeping of the speculated leaf, while its successor is being swept
   __device__ int act_spec_book() {
     FITOCT_MARK(act_spec_book);
+    if (!helped) spec_weight();   // no helper wave in a tile of several chains
     const int r = leaf_book_split(k_q, k_pe, k_g, k_minv, k_lp, k_s2);
     if (r == LB_NEXT) {   // the rest of act_begin_subtree (the top merge set depth d + 1)
       Sp->dir = k_dirn;
@@ -1596,6 +1598,8 @@ struct Chain {
       if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;
       Sp->lf_e = k_en;
     }
+    // without a helper, the next position's prior part follows the bookkeeping here
+    if (!helped && r != LB_END) prior_and_uniforms(true, k_dn, k_jn, k_t);
     return r == LB_END ? A_SPEC_DISCARD : A_SPEC_WAIT;
   }
 
@@ -1667,16 +1671,18 @@ struct Chain {
       persist = crit3(far, p, rtot, far, Tpb, rx, near, p, ry, minv);
     }
     sub(2, ts);
-    // phase B: the helper's weight of this leaf
-    long long spins = 0;
-    while (*help_wdone < help_want) {
-      if (++spins > SPIN_LIMIT) {
-        Sp->status = ERR_TIMEOUT;
-        return LB_END;
+    // phase B: the helper's weight of this leaf (or this wave's own, act_spec_book)
+    if (helped) {
+      long long spins = 0;
+      while (*help_wdone < help_want) {
+        if (++spins > SPIN_LIMIT) {
+          Sp->status = ERR_TIMEOUT;
+          return LB_END;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_s_sleep(1);
+      wave_fence();
     }
-    wave_fence();
     const double h = Sp->spec_h, wl = Sp->spec_wl;
     const XF wleaf{Sp->spec_wm, uni(Sp->spec_we)};
     Sp->sum_metro = sum_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
@@ -2134,7 +2140,10 @@ struct Chain {
         case A_LEAPFROG: a = act_leapfrog(); break;
         case A_WRITE_MP: a = act_write_mp(); break;
         case A_PRIOR: a = act_prior(); break;
-        case A_SPEC_BOOK: a = act_spec_book(); break;
+        case A_SPEC_BOOK:
+          if constexpr (spec) a = act_spec_book();   // only the SPEC sampler carries this code
+          else a = A_YIELD;
+          break;
         default: a = A_YIELD; break;
       }
       if (prof) {
@@ -2259,7 +2268,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   // request {depth, leaf, iteration} for the prior part of a speculated position; the
   // helper wave (slot 1) runs it and publishes the request number it finished
   __shared__ int help_req, help_done, help_wdone, help_arg[3];
-  const bool spec = SPEC && !MIG && nct == 1;
+  const bool spec = SPEC && !MIG;
+  const bool helped = spec && nct == 1;   // a spare NUTS wave helps the tile's one chain
 
   load_kinv<PPL, NNP>(P, L, tid);
   if (tid == 0) {
@@ -2369,7 +2379,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     }
     const int c = wave - NGW;
     const bool mig = MIG && P.mig != nullptr;
-    if (spec && c == 1) {   // the helper wave of slot 0's chain
+    if (helped && c == 1) {   // the helper wave of slot 0's chain
       using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
       Ch ch(P, L, 0, c0, lane, nct);
       int seen = 0;
@@ -2420,17 +2430,21 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
             __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
                              __ATOMIC_RELAXED);
-            help_arg[0] = ch.k_dn;
-            help_arg[1] = ch.k_jn;
-            help_arg[2] = (int)ch.k_t;
-            wave_fence();   // the arguments land before the request number
-            __atomic_store_n(&help_req, hreq + 1, __ATOMIC_RELAXED);
+            if (helped) {
+              help_arg[0] = ch.k_dn;
+              help_arg[1] = ch.k_jn;
+              help_arg[2] = (int)ch.k_t;
+              wave_fence();   // the arguments land before the request number
+              __atomic_store_n(&help_req, hreq + 1, __ATOMIC_RELAXED);
+            }
           }
           if (stamp) t_enq = (long long)__builtin_amdgcn_s_memtime();
-          ++hreq;
+          if (helped) {
+            ++hreq;
+            ch.help_wdone = (volatile AS_LDS int*)&help_wdone;
+            ch.help_want = hreq;
+          }
           ++epoch;
-          ch.help_wdone = (volatile AS_LDS int*)&help_wdone;
-          ch.help_want = hreq;
           a = Ch::A_SPEC_BOOK;
           continue;
         }
@@ -2512,7 +2526,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
                       (unsigned long long)__builtin_amdgcn_s_memrealtime());
             atomicAdd(&chains_done_here, 1);
           }
-          if (spec && lane == 0) __atomic_store_n(&help_req, -1, __ATOMIC_RELAXED);   // release the helper
+          if (helped && lane == 0) __atomic_store_n(&help_req, -1, __ATOMIC_RELAXED);   // release the helper
           break;
         }
         if (++steps > P.max_steps) {   // termination guarantee: report, never hang

@@ -142,8 +142,10 @@ typedef struct fitoct_plan_info {
 
 /* fitoct_plan_info::sampler.  PLAIN: tiles of several chains, or migration off;
  * MIGRATE: chains move between tiles at transition boundaries (work balance);
- * SPECULATIVE: one chain per tile, whose next leapfrog position is swept while the
- * current leaf's tree bookkeeping runs (FITOCT_NO_SPEC=1 turns it off).  The draws
+ * SPECULATIVE: one chain per tile (or FITOCT_SPEC=1 on any plan without migration);
+ * each chain's next leapfrog position is swept while the current leaf's tree
+ * bookkeeping runs, with a spare wave's help in a tile of one chain (FITOCT_NO_SPEC=1
+ * turns it off).  The draws
  * are the same bit for bit whichever variant runs. */
 #define FITOCT_SAMPLER_PLAIN 0
 #define FITOCT_SAMPLER_MIGRATE 1

@@ -2,7 +2,8 @@
 with one chain per tile the next leapfrog position is swept while the current leaf's
 merges and U-turn checks run, and a helper wave computes its prior part.  The draws
 must equal the plain sampler's (FITOCT_NO_SPEC=1) bit for bit, trajectory ends
-(discarded speculations) included, for every prior family."""
+(discarded speculations) included, for every prior family; likewise in tiles of
+several chains that do not migrate, where there is no helper wave."""
 from __future__ import annotations
 
 import os
@@ -45,8 +46,49 @@ def test_speculative_leaves_preserve_draws_bitwise(family, N, depth):
     assert a.total_leapfrogs == b.total_leapfrogs
 
 
-def test_tiles_of_several_chains_do_not_speculate():
+def test_migrating_plans_do_not_speculate():
     prob = _prob("normal", 512, 15)
     cfg = SamplerConfig(chains=1024, warmup=10, samples=10, seed=3, max_treedepth=6)
     with Plan(prob, cfg) as pl:
-        assert pl.info["chains_per_tile"] == 4 and pl.info["sampler"] != 2
+        assert pl.info["chains_per_tile"] == 4 and pl.info["sampler"] == 1   # MIGRATE
+
+
+def test_tiles_of_several_chains_speculate_without_helper_bitwise():
+    """With FITOCT_SPEC=1 and no migration, tiles of four chains take the speculative
+    path with no helper wave: each chain's wave computes the weight and the next prior
+    part itself (not the default: it is slower there).  Same draws as the plain sampler."""
+    prob = _prob("horseshoe", 512, 15)
+    cfg = SamplerConfig(chains=1024, warmup=40, samples=30, seed=5, max_treedepth=7)
+    old = {k: os.environ.get(k) for k in ("FITOCT_NO_MIGRATE", "FITOCT_SPEC")}
+    os.environ["FITOCT_NO_MIGRATE"] = "1"
+    os.environ["FITOCT_SPEC"] = "1"
+    try:
+        info, a = _run(prob, cfg, spec=True)
+        info0, b = _run(prob, cfg, spec=False)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert info["chains_per_tile"] == 4
+    assert info["sampler"] == 2 and info0["sampler"] == 0
+    np.testing.assert_array_equal(a.draws, b.draws)
+    assert a.total_leapfrogs == b.total_leapfrogs
+
+
+def test_batch_speculates_bitwise():
+    from fitoct_amd import sample_batch
+    probs = [_prob("normal", 481, 15, seed=40 + f) for f in range(6)]
+    cfg = SamplerConfig(chains=4, warmup=40, samples=30, seed=9)
+    old = os.environ.pop("FITOCT_NO_SPEC", None)
+    try:
+        a = sample_batch(probs, cfg)
+        os.environ["FITOCT_NO_SPEC"] = "1"
+        b = sample_batch(probs, cfg)
+    finally:
+        os.environ.pop("FITOCT_NO_SPEC", None)
+        if old is not None:
+            os.environ["FITOCT_NO_SPEC"] = old
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x.draws, y.draws)
