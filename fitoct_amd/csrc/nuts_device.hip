@@ -96,7 +96,6 @@ enum VecId : int {
   V_RHO, V_PNEAR,              // trajectory momentum sum, near end of old trajectory
   V_QS, V_QE,                  // staged q and its constrained values (exp on positive params)
   V_PG, V_CA,                  // prior part of grad, likelihood coefficient (prior_part)
-  V_SPEC_PE,                   // speculative path: the booked leaf's end-updated momentum
   NVEC
 };
 // U-turn record of one tree level (LDS)
@@ -113,14 +112,14 @@ struct ChainScalars {
   int st_w_e[MAXDEPTH];
   double H0, lsw_m, sum_metro, eps, eps_used, mu, s_bar, x_bar, ss_H0, lf_e;
   double cur_lp, cur_s2, smp_lp, smp_s2;
-  double pr_lp, pr_is2, u_top, spec_lp;
+  double pr_lp, pr_is2, u_top, spec_wm;   // spec_wm, spec_we, spec_h: the speculative
+                                          // path's booked leaf weight and energy
   int u_blk[MAXDEPTH];     // which block of 64 merge uniforms each level's ring holds (-1: none)
   double end_lp[2], end_s2[2];
   double st_w_m[MAXDEPTH];
   double pool_lp[MAXDEPTH + 1], pool_s2[MAXDEPTH + 1];
-  double spec_h, spec_wl, spec_wm, pad5;   // speculative path: the booked leaf's energy and weight
   long long leapfrogs;
-  long long pad3;
+  double spec_h;
   long long prof[2][32];   // diagnostic build: cycles and calls per action
 };
 static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
@@ -1576,8 +1575,9 @@ struct Chain {
       en = dirn ? Sp->eps_used : -Sp->eps_used;
     }
     leapfrog_stage(qs, ps, gs, minv, en);
-    st(V_SPEC_PE, pe);   // for the helper: this leaf's energy and weight (spec_weight)
-    Sp->spec_lp = cur_lp;
+    // for the helper (spec_weight): the booked leaf's end-updated momentum, in CUR_G's
+    // slot (while a tree grows nothing reads CUR_G; begin_subtree rewrites it)
+    st(V_CUR_G, pe);   // (its lp is Sp->cur_lp, set by act_grad)
     k_q = q; k_pe = pe; k_g = g; k_minv = minv; k_ps = ps; k_gs = gs;
     k_lp = cur_lp; k_s2 = cur_s2; k_en = en;
     k_dirn = dirn; k_dn = dn; k_jn = jn; k_t = t;
@@ -1606,13 +1606,11 @@ struct Chain {
   // run by the helper wave for the leaf being booked: its Hamiltonian and multinomial
   // weight, the same operations as leaf_book's first lines
   __device__ void spec_weight() const {
-    const V pe = ld(V_SPEC_PE), minv = ld(V_MINV);
-    double h = -Sp->spec_lp + kin(pe, minv);
+    const V pe = ld(V_CUR_G), minv = ld(V_MINV);   // leaf_spec staged the momentum there
+    double h = -Sp->cur_lp + kin(pe, minv);
     if (isnan(h)) h = INFINITY;
-    const double wl = Sp->H0 - h;
-    const XF w = xf_exp(wl);
+    const XF w = xf_exp(Sp->H0 - h);
     Sp->spec_h = h;
-    Sp->spec_wl = wl;
     Sp->spec_wm = w.m;
     Sp->spec_we = w.e;
   }
@@ -1683,7 +1681,7 @@ struct Chain {
       }
       wave_fence();
     }
-    const double h = Sp->spec_h, wl = Sp->spec_wl;
+    const double h = Sp->spec_h, wl = H0 - h;
     const XF wleaf{Sp->spec_wm, uni(Sp->spec_we)};
     Sp->sum_metro = sum_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
     sub(1, ts);
@@ -2140,10 +2138,7 @@ struct Chain {
         case A_LEAPFROG: a = act_leapfrog(); break;
         case A_WRITE_MP: a = act_write_mp(); break;
         case A_PRIOR: a = act_prior(); break;
-        case A_SPEC_BOOK:
-          if constexpr (spec) a = act_spec_book();   // only the SPEC sampler carries this code
-          else a = A_YIELD;
-          break;
+        case A_SPEC_BOOK: a = act_spec_book(); break;
         default: a = A_YIELD; break;
       }
       if (prof) {
