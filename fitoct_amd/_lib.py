@@ -137,6 +137,7 @@ SIGNATURES = [
                                      C.POINTER(C.c_int32)]),
     ("fitoct_plan_cancel", C.c_int32, [C.c_void_p]),
     ("fitoct_plan_wait", C.c_int32, [C.c_void_p]),
+    ("fitoct_plan_set_init", C.c_int32, [C.c_void_p, _dp, _dp, _dp]),
     ("fitoct_plan_download", C.c_int32, [C.c_void_p, C.POINTER(Result)]),
     ("fitoct_plan_destroy", None, [C.c_void_p]),
     ("fitoct_batch_create", C.c_int32,
@@ -197,7 +198,7 @@ def _single_hip_runtime():
         pass
 
 
-ABI_VERSION = 2   # include/fitoct.h FITOCT_ABI_VERSION
+ABI_VERSION = 3   # include/fitoct.h FITOCT_ABI_VERSION
 
 
 def lib():

@@ -226,6 +226,25 @@ class Plan:
             raise
         self.wait()
 
+    def set_init(self, q_init=None, stepsize=None, inv_metric=None):
+        """Warm restart (``fitoct_plan_set_init``): per-chain start position q_init
+        [chains, D] (unconstrained), initial step size [chains] and diagonal inverse
+        metric [chains, D] for the next runs; None keeps the default (jittered start
+        around theta0, ``cfg.stepsize``, unit metric).  A previous run's ``last_q``,
+        ``stepsize`` and ``inv_metric`` resume it (``adapt_engaged=False`` keeps them)."""
+        C_, D = self.info["chains"], self.info["dim"]
+        self._init = []   # kept alive only for the call (the library copies them)
+
+        def arr(a, shape):
+            if a is None:
+                return None
+            a = np.ascontiguousarray(np.broadcast_to(np.asarray(a, dtype=np.float64), shape))
+            self._init.append(a)
+            return dptr(a)
+        check(lib().fitoct_plan_set_init(self._h, arr(q_init, (C_, D)), arr(stepsize, (C_,)),
+                                         arr(inv_metric, (C_, D))))
+        self._init = []
+
     def launch(self, d_draws: int = 0, stream: int = 0):
         """Enqueue the run and return at once (see :meth:`poll`, :meth:`wait`)."""
         check(lib().fitoct_plan_launch(self._h, C.c_void_p(d_draws or None),
@@ -365,10 +384,15 @@ def sample_batch(probs, cfg: SamplerConfig):
     return outs
 
 
-def sample(prob: ExpGPProblem, cfg: SamplerConfig, progress=None) -> SampleOutput:
-    """One-shot sampler run (plan + run + download); ``progress`` as in :meth:`Plan.run`."""
+def sample(prob: ExpGPProblem, cfg: SamplerConfig, progress=None,
+           resume: SampleOutput | None = None) -> SampleOutput:
+    """One-shot sampler run (plan + run + download); ``progress`` as in :meth:`Plan.run`.
+    ``resume``: a previous run of the same chains whose last position, step size and
+    inverse metric start this one (:meth:`Plan.set_init`)."""
     t0 = time.perf_counter()
     with Plan(prob, cfg) as pl:
+        if resume is not None:
+            pl.set_init(resume.last_q, resume.stepsize, resume.inv_metric)
         pl.run(progress=progress)
         out = pl.download()
     out.wall_ms = (time.perf_counter() - t0) * 1e3

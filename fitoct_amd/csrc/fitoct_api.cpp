@@ -66,6 +66,7 @@ struct fitoct_plan {
   double* d_draws = nullptr;  // internal draws buffer (lazily allocated)
   double* d_stack = nullptr;
   double* d_fin = nullptr;    // eps[C] | minv[C*D] | q[C*D]
+  double* d_init = nullptr;   // warm restart (fitoct_plan_set_init): eps[C] | minv[C*D] | q[C*D]
   int* d_status = nullptr;
   long long* d_leap = nullptr;
   KParams* d_kp = nullptr;    // device copy of the launch parameters
@@ -443,6 +444,7 @@ void free_plan(fitoct_plan* pl) {
   (void)hipFree(pl->d_draws);
   (void)hipFree(pl->d_stack);
   (void)hipFree(pl->d_fin);
+  (void)hipFree(pl->d_init);
   (void)hipFree(pl->d_status);
   (void)hipFree(pl->d_leap);
   (void)hipFree(pl->d_kp);
@@ -789,6 +791,41 @@ int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
     info->lds_bytes = pl->lds;
     info->n_pad = pl->kp.n_pad;
     info->draws_bytes = (int64_t)pl->draws_bytes;
+    return FITOCT_OK;
+  });
+}
+
+int32_t fitoct_plan_set_init(fitoct_plan* pl, const double* q_init, const double* stepsize,
+                             const double* inv_metric) {
+  return guarded(__func__, [&]() -> int32_t {
+    if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    if (pl->launched) return fail(FITOCT_E_ARG, "plan is running: call fitoct_plan_wait first");
+    const int C = pl->kp.chains, D = pl->kp.D;
+    // checked on the host: the kernel takes every value as given
+    if (stepsize)
+      for (int c = 0; c < C; ++c)
+        if (!(stepsize[c] > 0.0 && stepsize[c] < INFINITY))
+          return fail(FITOCT_E_ARG, "stepsize must be finite and > 0");
+    if (inv_metric)
+      for (size_t i = 0; i < (size_t)C * D; ++i)
+        if (!(inv_metric[i] > 0.0 && inv_metric[i] < INFINITY))
+          return fail(FITOCT_E_ARG, "inv_metric must be finite and > 0");
+    if (q_init)
+      for (size_t i = 0; i < (size_t)C * D; ++i)
+        if (!isfinite(q_init[i])) return fail(FITOCT_E_ARG, "q_init must be finite");
+    HIP_TRY(hipSetDevice(pl->cfg.device));
+    if ((q_init || stepsize || inv_metric) && !pl->d_init)
+      HIP_TRY(hipMalloc(&pl->d_init, sizeof(double) * (size_t)C * (1 + 2 * D)));
+    double* d_eps = pl->d_init;
+    double* d_minv = pl->d_init ? pl->d_init + C : nullptr;
+    double* d_q = pl->d_init ? pl->d_init + C + (size_t)C * D : nullptr;
+    if (stepsize) HIP_TRY(hipMemcpy(d_eps, stepsize, sizeof(double) * C, hipMemcpyHostToDevice));
+    if (inv_metric)
+      HIP_TRY(hipMemcpy(d_minv, inv_metric, sizeof(double) * C * D, hipMemcpyHostToDevice));
+    if (q_init) HIP_TRY(hipMemcpy(d_q, q_init, sizeof(double) * C * D, hipMemcpyHostToDevice));
+    pl->kp.init_eps = stepsize ? d_eps : nullptr;
+    pl->kp.init_minv = inv_metric ? d_minv : nullptr;
+    pl->kp.init_q = q_init ? d_q : nullptr;
     return FITOCT_OK;
   });
 }

@@ -76,6 +76,11 @@ struct KParams {
   double adapt_delta, gamma, kappa, t0, stepsize0, init_radius;
   int init_buffer, term_buffer, base_window;
   long long max_steps;      // per-tile step bound (termination guarantee)
+  // warm restart (fitoct_plan_set_init; nullptr: defaults): per-chain initial step size,
+  // diagonal inverse metric and unconstrained position, indexed by the launch's chain
+  const double* init_eps;   // [chains]
+  const double* init_minv;  // [chains][D]
+  const double* init_q;     // [chains][D]
   // ---- outputs ----
   double* draws;            // [chains][iters_saved][ncols]
   int ncols, iters_saved;

@@ -1286,13 +1286,22 @@ struct Chain {
     Sp->prof[lane >> 5][lane & 31] = 0;
 #pragma unroll 1
     for (int v = 0; v < NVEC; ++v) st(v, zero);
-    st(V_MINV, one);
+    if (Pr().init_minv) {   // warm restart (fitoct_plan_set_init): the chain's metric
+      V m;
+#pragma unroll
+      for (int s = 0; s < PPL; ++s)
+        m.a[s] = ok(s) ? Pr().init_minv[(size_t)lc * Pr().D + idx(s)] : 0.0;
+      st(V_MINV, m);
+    } else {
+      st(V_MINV, one);
+    }
     if (lane < NSLOT) SUMS[lane] = 0.0;
     AUX[lane] = 0.0;
     Sp->status = 0;
     Sp->leapfrogs = 0;
-    Sp->eps = Pr().stepsize0;
-    Sp->mu = log(10.0 * Pr().stepsize0);
+    const double eps0 = Pr().init_eps ? Pr().init_eps[lc] : Pr().stepsize0;
+    Sp->eps = eps0;
+    Sp->mu = log(10.0 * eps0);
     Sp->da_counter = 0;
     Sp->s_bar = 0.0;
     Sp->x_bar = 0.0;
@@ -1338,6 +1347,7 @@ struct Chain {
       }
       const double u = uniform(key, (uint32_t)attempt, TAG_INIT, (uint32_t)k, 0u);
       q.a[s] = (k < Pr().D) ? base + Pr().init_radius * w * (2.0 * u - 1.0) : 0.0;
+      if (Pr().init_q && k < Pr().D) q.a[s] = Pr().init_q[(size_t)lc * Pr().D + k];   // warm restart
     }
     st(V_CUR_Q, q);
     Sp->state = ST_INIT;
@@ -1353,7 +1363,7 @@ struct Chain {
       if (ok(s) && !(fabs(g.a[s]) <= DBL_MAX)) bad = 1.0;
     bad = wave_sum(bad);
     if (!(Sp->cur_lp > -INFINITY) || bad != 0.0) {
-      if (Sp->init_attempt + 1 >= 100) {
+      if (Sp->init_attempt + 1 >= 100 || Pr().init_q) {   // a given start is not retried
         Sp->status = ERR_INIT;
         return A_FINISH;
       }

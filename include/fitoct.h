@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FITOCT_ABI_VERSION 2
+#define FITOCT_ABI_VERSION 3
 /* largest accepted N (depth bins): bounds every host and device allocation derived from it */
 #define FITOCT_MAX_BINS (1 << 22)
 
@@ -216,6 +216,20 @@ int32_t fitoct_plan_poll(fitoct_plan* plan, int64_t* iterations_done, int64_t* i
                          int32_t* finished);
 int32_t fitoct_plan_cancel(fitoct_plan* plan);
 int32_t fitoct_plan_wait(fitoct_plan* plan);
+/* Warm restart (SURVEY.md §5 "Checkpoint / resume"; rstan::sampling's `init`, `control =
+ * list(stepsize)` and CmdStan's `inv_metric`): per-chain starting values for the plan's
+ * next runs, host buffers copied at once (NULL = keep that default):
+ *   q_init     [chains][D] unconstrained positions, e.g. a previous run's last_q;
+ *   stepsize   [chains] initial step sizes (> 0), e.g. its stepsize;
+ *   inv_metric [chains][D] diagonal inverse metrics (> 0), e.g. its inv_metric.
+ * Defaults: the jittered start around theta0 (init_radius), cfg.stepsize, a unit metric.
+ * With adapt_engaged = 0 the chains sample with that step size and metric unchanged; with
+ * adaptation they are where Stan's adaptation starts (step-size search, windows).  A chain
+ * whose q_init has a non-finite lp / gradient fails with FITOCT_E_INIT (no retry: Stan
+ * rejects a user init likewise).  A NULL argument clears that input.  Not while a launch
+ * is in flight (FITOCT_E_ARG). */
+int32_t fitoct_plan_set_init(fitoct_plan* plan, const double* q_init, const double* stepsize,
+                             const double* inv_metric);
 /* Copy the last run's outputs to host buffers of `res`. */
 int32_t fitoct_plan_download(fitoct_plan* plan, fitoct_result* res);
 void fitoct_plan_destroy(fitoct_plan* plan);

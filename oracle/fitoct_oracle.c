@@ -626,6 +626,17 @@ static int init_stepsize(nuts_ctx* c, ps_point* z, uint32_t window, double* eps)
   return rc;
 }
 
+/* warm restart (oracle_set_init, the restatement of fitoct_plan_set_init): per-chain
+ * initial step size [chains], inverse metric [chains][D] and position [chains][D] of the
+ * next oracle_sample calls; NULL = the defaults below.  Caller-owned, read-only. */
+static const double *g_init_eps, *g_init_minv, *g_init_q;
+
+void oracle_set_init(const double* q_init, const double* stepsize, const double* inv_metric) {
+  g_init_q = q_init;
+  g_init_eps = stepsize;
+  g_init_minv = inv_metric;
+}
+
 /* one chain: init, adaptation (adapt_diag_e_nuts), sampling */
 static int run_chain(const model* m, const fitoct_config* cfg, int lc, double* draws, int ncols,
                      int iters_saved, double* out_eps, double* out_minv, long long* out_lf) {
@@ -639,7 +650,7 @@ static int run_chain(const model* m, const fitoct_config* cfg, int lc, double* d
   c.minv = (double*)malloc(sizeof(double) * D);
   c.work = (double*)malloc(sizeof(double) * 3 * (Nn + 1));
   pt_alloc(&c.z, D);
-  for (int k = 0; k < D; ++k) c.minv[k] = 1.0;
+  for (int k = 0; k < D; ++k) c.minv[k] = g_init_minv ? g_init_minv[(size_t)lc * D + k] : 1.0;
   ps_point z;
   pt_alloc(&z, D);
   /* initial point: jitter around theta0 (inits) */
@@ -657,19 +668,20 @@ static int run_chain(const model* m, const fitoct_config* cfg, int lc, double* d
         if (m->fam == 0 && k == 3 + Nn) base = -log(m->rate);
       }
       z.q[k] = base + cfg->init_radius * w * (2.0 * unif(c.key, (uint32_t)attempt, T_INIT, (uint32_t)k, 0u) - 1.0);
+      if (g_init_q) z.q[k] = g_init_q[(size_t)lc * D + k];
     }
     z.lp = logp_grad(m, z.q, z.g, &z.s2, c.work);
     int finite = z.lp > -INFINITY;
     for (int k = 0; k < D; ++k) finite = finite && isfinite(z.g[k]);
     if (finite) break;
-    if (attempt + 1 >= 100) {
+    if (attempt + 1 >= 100 || g_init_q) { /* a given start is not retried */
       rc = FITOCT_E_INIT;
       break;
     }
   }
-  double eps = cfg->stepsize;
+  double eps = g_init_eps ? g_init_eps[lc] : cfg->stepsize;
   /* dual averaging */
-  double mu = log(10 * cfg->stepsize), s_bar = 0, x_bar = 0;
+  double mu = log(10 * eps), s_bar = 0, x_bar = 0;
   int da_n = 0;
   /* windowed adaptation */
   int ib = cfg->init_buffer, tb = cfg->term_buffer, bw = cfg->window;

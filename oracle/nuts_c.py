@@ -48,6 +48,8 @@ def lib():
                                     C.POINTER(C.c_uint32)]
         L.oracle_normals.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_int, dp]
+        L.oracle_set_init.argtypes = [dp, dp, dp]
+        L.oracle_set_init.restype = None
         _L = L
     return _L
 
@@ -87,17 +89,25 @@ def logp_grad(prob, q):
     return lp, g, s2
 
 
-def sample(prob, cfg, nthreads: int = 0):
-    """prob: ExpGPProblem, cfg: SamplerConfig -> dict(draws, stepsize, inv_metric, leapfrogs)."""
+def sample(prob, cfg, nthreads: int = 0, q_init=None, init_stepsize=None, init_inv_metric=None):
+    """prob: ExpGPProblem, cfg: SamplerConfig -> dict(draws, stepsize, inv_metric, leapfrogs).
+    q_init [chains, D] / init_stepsize [chains] / init_inv_metric [chains, D]: the warm
+    restart of fitoct_plan_set_init (None = the default start)."""
     D = prob.D
+    arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float64)
+            for a in (q_init, init_stepsize, init_inv_metric)]
     iters = cfg.warmup + cfg.samples if cfg.save_warmup else cfg.samples
     draws = np.full((cfg.chains, iters, D + 8), np.nan)
     eps = np.zeros(cfg.chains)
     minv = np.zeros((cfg.chains, D))
     lf = np.zeros(cfg.chains, dtype=np.int64)
     p, c = prob.to_c(), cfg.to_c()
-    rc = lib().oracle_sample(C.byref(p), C.byref(c), _dp(draws), _dp(eps), _dp(minv),
-                             lf.ctypes.data_as(C.POINTER(C.c_longlong)), int(nthreads))
+    lib().oracle_set_init(*[None if a is None else _dp(a) for a in arrs])
+    try:
+        rc = lib().oracle_sample(C.byref(p), C.byref(c), _dp(draws), _dp(eps), _dp(minv),
+                                 lf.ctypes.data_as(C.POINTER(C.c_longlong)), int(nthreads))
+    finally:
+        lib().oracle_set_init(None, None, None)
     if rc != 0:
         raise RuntimeError(f"oracle_sample failed with status {rc}")
     return {"draws": draws, "stepsize": eps, "inv_metric": minv, "leapfrogs": lf}

@@ -46,7 +46,7 @@ def test_struct_layouts_match_ctypes():
     sizes = _lib.struct_sizes()
     assert sizes == (C.sizeof(_lib.Problem), C.sizeof(_lib.Config), C.sizeof(_lib.Result),
                      C.sizeof(_lib.PlanInfo))
-    assert _lib.lib().fitoct_abi_version() == 2
+    assert _lib.lib().fitoct_abi_version() == 3
 
 
 def test_default_config_is_stan_default():
@@ -216,3 +216,10 @@ def test_oversize_n_rejected():
     out = np.empty(3)
     assert _lib.lib().fitoct_mono_initial_theta(max_bins + 1, _lib.dptr(x), _lib.dptr(x), 2,
                                                 _lib.dptr(out)) == -1
+
+
+def test_set_init_needs_a_plan():
+    """fitoct_plan_set_init (warm restart) reports a NULL plan as FITOCT_E_ARG."""
+    L = _lib.lib()
+    assert L.fitoct_plan_set_init(None, None, None, None) == -1
+    assert b"plan" in L.fitoct_last_error()

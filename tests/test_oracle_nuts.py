@@ -91,3 +91,39 @@ def test_sampler_columns_consistent():
     assert np.all(d[..., c["sigma"]] > 0) and np.all(d[..., c["theta.3"]] > 0)
     assert np.all(d[..., c["br"]] >= 0)
     assert np.all(td <= cfg.max_treedepth)
+
+
+def test_warm_restart_restatement():
+    """oracle_set_init (the restatement of fitoct_plan_set_init): with adaptation off the
+    given step size and metric are used unchanged, the chains start at the given point
+    (no jittered init: the run does not depend on init_radius), a start whose density is
+    not finite fails with FITOCT_E_INIT instead of being retried, and clearing the start
+    restores the default run."""
+    prob = _small()
+    first = nuts_c.sample(prob, SamplerConfig(chains=4, warmup=150, samples=20, seed=3),
+                          nthreads=4)
+    last = first["draws"][:, -1, 7:7 + prob.D]
+    logc = np.array([k < 3 or k >= 3 + prob.Nn for k in range(prob.D)])
+    q0 = last.copy()
+    q0[:, logc] = np.log(last[:, logc])
+    cfg = SamplerConfig(chains=4, warmup=0, samples=30, seed=4, adapt_engaged=False)
+    kw = dict(q_init=q0, init_stepsize=first["stepsize"], init_inv_metric=first["inv_metric"])
+    a = nuts_c.sample(prob, cfg, nthreads=4, **kw)
+    cfg_r = SamplerConfig(chains=4, warmup=0, samples=30, seed=4, adapt_engaged=False,
+                          init_radius=0.5)
+    b = nuts_c.sample(prob, cfg_r, nthreads=4, **kw)
+    assert np.array_equal(a["draws"], b["draws"], equal_nan=True)
+    assert np.array_equal(a["stepsize"], first["stepsize"])
+    assert np.array_equal(a["inv_metric"], first["inv_metric"])
+    assert np.all(a["draws"][:, :, 2] == first["stepsize"][:, None])
+    # started in the typical set: lp__ of the first draws matches the first run's tail
+    tail = first["draws"][:, -20:, 0]
+    assert abs(a["draws"][:, :5, 0].mean() - tail.mean()) < 5.0 * tail.std()
+    bad = q0.copy()
+    bad[1, 0] = 800.0   # theta1 = exp(800): lp = -inf
+    with pytest.raises(RuntimeError, match="status -4"):
+        nuts_c.sample(prob, cfg, nthreads=4, q_init=bad)
+    d0 = nuts_c.sample(prob, cfg, nthreads=4)
+    d1 = nuts_c.sample(prob, cfg, nthreads=4)
+    assert np.array_equal(d0["draws"], d1["draws"], equal_nan=True)
+    assert not np.array_equal(d0["draws"], a["draws"], equal_nan=True)
