@@ -41,10 +41,17 @@ def _gather_rows(t, world, rank, dst=0):
     return out
 
 
-def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=None):
+def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=None,
+                   resume: SampleOutput | None = None):
     """Run ``cfg.chains`` global chains split over the process group; rank 0
     returns the full :class:`SampleOutput` (chains in global order), other ranks
     return their local output without draws.
+
+    ``resume`` (warm restart, :meth:`fitoct_amd.api.Plan.set_init`): a previous run of
+    the same global chains (e.g. this function's rank-0 output, available on every
+    rank); each rank starts its block from that run's last positions, step sizes and
+    inverse metrics.  With ``engine`` they reach it as ``engine(prob, cfg, init=(q,
+    stepsize, inv_metric))``.
 
     Without ``engine`` each rank's HIP plan writes its draws into a device tensor;
     with the ``nccl`` backend that tensor is gathered over RCCL directly, with
@@ -61,11 +68,19 @@ def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=N
     if count == 0:
         raise ValueError(f"rank {rank} has no chains ({cfg.chains} chains over {world} ranks)")
     local = replace(cfg, chains=count, chain_offset=cfg.chain_offset + offset)
+    init = None
+    if resume is not None:
+        if len(resume.stepsize) != cfg.chains or resume.last_q.shape != (cfg.chains, prob.D):
+            raise ValueError("resume must hold the cfg.chains chains of a previous run")
+        blk = slice(offset, offset + count)
+        init = (resume.last_q[blk], resume.stepsize[blk], resume.inv_metric[blk])
     nccl = dist.get_backend() == "nccl"
     if engine is None:
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         local = replace(local, device=dev.index)
         with Plan(prob, local) as pl:
+            if init is not None:
+                pl.set_init(*init)
             info = pl.info
             iters, ncols = info["iters_saved"], info["n_cols"]
             buf = torch.zeros((cmax, iters, ncols), dtype=torch.float64, device=dev)
@@ -75,7 +90,7 @@ def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=N
             torch.cuda.current_stream(dev).synchronize()
             buf, dev = buf.cpu(), torch.device("cpu")
     else:
-        out = engine(prob, local)
+        out = engine(prob, local) if init is None else engine(prob, local, init=init)
         iters, ncols = out.draws.shape[1:]
         buf = torch.zeros((cmax, iters, ncols), dtype=torch.float64)
         buf[:count] = torch.from_numpy(out.draws)

@@ -45,10 +45,12 @@ def _problem():
                         Sigma0=S0, prior_type="lasso")
 
 
-def _oracle_engine(prob, cfg):
+def _oracle_engine(prob, cfg, init=None):
     from fitoct_amd.api import SampleOutput
     from oracle import nuts_c
-    o = nuts_c.sample(prob, cfg, nthreads=1)
+    kw = {} if init is None else dict(q_init=init[0], init_stepsize=init[1],
+                                      init_inv_metric=init[2])
+    o = nuts_c.sample(prob, cfg, nthreads=1, **kw)
     return SampleOutput(o["draws"], prob.column_names(), cfg.warmup, o["stepsize"],
                         o["inv_metric"], np.zeros_like(o["inv_metric"]),
                         int(o["leapfrogs"].sum()), 0.0, 0.0, cfg.chain_offset)
@@ -180,3 +182,85 @@ def test_hip_batch_sharded_gather_equals_single_batch(tmp_path):
     ref = sample_batch(_batch_problems(), SamplerConfig(chains=2, warmup=20, samples=10, seed=5,
                                                         max_treedepth=5))
     np.testing.assert_array_equal(got, np.stack([o.draws for o in ref]))
+
+
+def _resume_state(chains):
+    """A previous run's end state for every global chain (oracle run, last draw mapped
+    back to the unconstrained space)."""
+    from fitoct_amd.api import SampleOutput, SamplerConfig
+    prob = _problem()
+    o = _oracle_engine(prob, SamplerConfig(chains=chains, warmup=40, samples=10, seed=3,
+                                           max_treedepth=5))
+    last = o.draws[:, -1, 7:7 + prob.D]
+    logc = np.array([k < 3 or k >= 3 + prob.Nn for k in range(prob.D)])
+    q = last.copy()
+    q[:, logc] = np.log(last[:, logc])
+    return SampleOutput(None, [], 0, o.stepsize, o.inv_metric, q, 0, 0.0, 0.0)
+
+
+def _resume_worker(rank, world, port, chains, outdir):
+    import torch.distributed as dist
+    from fitoct_amd.api import SamplerConfig
+    from fitoct_amd.distributed import sample_sharded
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        cfg = SamplerConfig(chains=chains, warmup=0, samples=20, seed=22, max_treedepth=5,
+                            adapt_engaged=False)
+        out = sample_sharded(_problem(), cfg, engine=_oracle_engine,
+                             resume=_resume_state(chains))
+        if rank == 0:
+            np.savez(os.path.join(outdir, "resumed.npz"), draws=out.draws, stepsize=out.stepsize)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_resume_equals_single_run(tmp_path):
+    """Warm restart over the process group: each rank starts its chain block from the
+    previous run's end state, and the gathered draws equal one process resuming all
+    chains (uneven split: 5 chains over 2 ranks)."""
+    from fitoct_amd.api import SamplerConfig
+    chains = 5
+    mp.spawn(_resume_worker, args=(2, _free_port(), chains, str(tmp_path)), nprocs=2,
+             join=True)
+    got = np.load(tmp_path / "resumed.npz")
+    st = _resume_state(chains)
+    ref = _oracle_engine(_problem(), SamplerConfig(chains=chains, warmup=0, samples=20, seed=22,
+                                                   max_treedepth=5, adapt_engaged=False),
+                         init=(st.last_q, st.stepsize, st.inv_metric))
+    np.testing.assert_array_equal(got["draws"], ref.draws)
+    np.testing.assert_array_equal(got["stepsize"], st.stepsize)
+
+
+def _hip_resume_worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    from fitoct_amd.api import SamplerConfig, sample
+    from fitoct_amd.distributed import sample_sharded
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        prev = sample(_gpu_problem(), SamplerConfig(chains=37, warmup=60, samples=10, seed=21,
+                                                    max_treedepth=6))
+        cfg = SamplerConfig(chains=37, warmup=0, samples=30, seed=23, max_treedepth=6,
+                            adapt_engaged=False)
+        out = sample_sharded(_gpu_problem(), cfg, resume=prev)
+        if rank == 0:
+            np.savez(os.path.join(outdir, "resumed.npz"), draws=out.draws)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_hip_plan_sharded_resume_equals_single_plan(tmp_path):
+    """Warm restart through the HIP plans of two ranks (37 chains: 19 + 18) equals one
+    plan resuming all chains, bit for bit."""
+    from fitoct_amd.api import SamplerConfig, sample
+    mp.spawn(_hip_resume_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    got = np.load(tmp_path / "resumed.npz")["draws"]
+    prev = sample(_gpu_problem(), SamplerConfig(chains=37, warmup=60, samples=10, seed=21,
+                                                max_treedepth=6))
+    ref = sample(_gpu_problem(), SamplerConfig(chains=37, warmup=0, samples=30, seed=23,
+                                               max_treedepth=6, adapt_engaged=False), resume=prev)
+    np.testing.assert_array_equal(got, ref.draws)
