@@ -1625,6 +1625,56 @@ struct Chain {
     Sp->spec_we = w.e;
   }
 
+  // base_nuts::transition's merge of the completed subtree of depth d (final weight Tw,
+  // proposal Tprop: -1 = the leaf (q, p, g) itself, else a pool slot) into the trajectory
+  // grown in direction dir: the new trajectory end, depth d + 1, the multinomial choice
+  // of the sample (u_top drawn by act_prior) and the trajectory weight.  Shared by
+  // leaf_book and leaf_book_split.
+  __device__ __forceinline__ void top_merge(const V& q, const V& p, const V& g, const double cur_lp,
+                                            const double cur_s2, const XF Tw, const int Tprop,
+                                            unsigned used, const int dir, const int d) const {
+    const XF Ww{Sp->lsw_m, Sp->lsw_e};
+    const double u_top = Sp->u_top;
+    const int eq = dir ? V_E1_Q : V_E0_Q;
+    st(eq, q);
+    st(eq + 1, p);
+    st(eq + 2, g);
+    Sp->end_lp[dir] = cur_lp;
+    Sp->end_s2[dir] = cur_s2;
+    Sp->depth = d + 1;
+    const bool take = xf_gt(Tw, Ww) || xf_u_below(u_top, Tw, Ww);
+    if (take) {
+      if (Tprop < 0) {
+        st(V_SMP_Q, q);
+        st(V_SMP_P, p);
+        st(V_SMP_G, g);
+        Sp->smp_lp = cur_lp;
+        Sp->smp_s2 = cur_s2;
+      } else {
+        const AS_GLB double* sq = pslot(Tprop, P_Q);
+        const AS_GLB double* sp = pslot(Tprop, P_P);
+        const AS_GLB double* sg = pslot(Tprop, P_G);
+        V q2, p2, g2;
+#pragma unroll
+        for (int s = 0; s < PPL; ++s) {
+          q2.a[s] = sq[idx(s)];
+          p2.a[s] = sp[idx(s)];
+          g2.a[s] = sg[idx(s)];
+        }
+        st(V_SMP_Q, q2);
+        st(V_SMP_P, p2);
+        st(V_SMP_G, g2);
+        Sp->smp_lp = Sp->pool_lp[Tprop];
+        Sp->smp_s2 = Sp->pool_s2[Tprop];
+      }
+    }
+    if (Tprop >= 0) used &= ~(1u << Tprop);
+    Sp->pool_used = (int)used;
+    const XF Wn = xf_add(Ww, Tw);
+    Sp->lsw_m = Wn.m;
+    Sp->lsw_e = Wn.e;
+  }
+
   // leaf_book for the speculative path, split so that the weight can come from the
   // helper wave: first every U-turn check the leaf completes (they need momenta only:
   // the running subtree's begin momentum and momentum sum follow the levels'
@@ -1736,46 +1786,7 @@ struct Chain {
       return LB_MID;
     }
     // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
-    const XF Ww{Sp->lsw_m, Sp->lsw_e};
-    const double u_top = Sp->u_top;
-    const int eq = dir ? V_E1_Q : V_E0_Q;
-    st(eq, q);
-    st(eq + 1, p);
-    st(eq + 2, g);
-    Sp->end_lp[dir] = cur_lp;
-    Sp->end_s2[dir] = cur_s2;
-    Sp->depth = d + 1;
-    const bool take = xf_gt(Tw, Ww) || xf_u_below(u_top, Tw, Ww);
-    if (take) {
-      if (Tprop < 0) {
-        st(V_SMP_Q, q);
-        st(V_SMP_P, p);
-        st(V_SMP_G, g);
-        Sp->smp_lp = cur_lp;
-        Sp->smp_s2 = cur_s2;
-      } else {
-        const AS_GLB double* sq = pslot(Tprop, P_Q);
-        const AS_GLB double* sp = pslot(Tprop, P_P);
-        const AS_GLB double* sg = pslot(Tprop, P_G);
-        V q2, p2, g2;
-#pragma unroll
-        for (int s = 0; s < PPL; ++s) {
-          q2.a[s] = sq[idx(s)];
-          p2.a[s] = sp[idx(s)];
-          g2.a[s] = sg[idx(s)];
-        }
-        st(V_SMP_Q, q2);
-        st(V_SMP_P, p2);
-        st(V_SMP_G, g2);
-        Sp->smp_lp = Sp->pool_lp[Tprop];
-        Sp->smp_s2 = Sp->pool_s2[Tprop];
-      }
-    }
-    if (Tprop >= 0) used &= ~(1u << Tprop);
-    Sp->pool_used = (int)used;
-    const XF Wn = xf_add(Ww, Tw);
-    Sp->lsw_m = Wn.m;
-    Sp->lsw_e = Wn.e;
+    top_merge(q, p, g, cur_lp, cur_s2, Tw, Tprop, used, dir, d);
     st(V_RHO, rtot);
     sub(3, ts);
     if (!persist || d + 1 >= Pr().max_depth) return LB_END;
@@ -1858,46 +1869,7 @@ struct Chain {
     }
     // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
     const int dir = uni(Sp->dir);
-    const XF Ww{Sp->lsw_m, Sp->lsw_e};
-    const double u_top = Sp->u_top;
-    const int eq = dir ? V_E1_Q : V_E0_Q;
-    st(eq, q);
-    st(eq + 1, p);
-    st(eq + 2, g);
-    Sp->end_lp[dir] = cur_lp;
-    Sp->end_s2[dir] = cur_s2;
-    Sp->depth = d + 1;
-    const bool take = xf_gt(Tw, Ww) || xf_u_below(u_top, Tw, Ww);   // u_top: drawn by act_prior
-    if (take) {
-      if (Tprop < 0) {
-        st(V_SMP_Q, q);
-        st(V_SMP_P, p);
-        st(V_SMP_G, g);
-        Sp->smp_lp = cur_lp;
-        Sp->smp_s2 = cur_s2;
-      } else {
-        const AS_GLB double* sq = pslot(Tprop, P_Q);
-        const AS_GLB double* sp = pslot(Tprop, P_P);
-        const AS_GLB double* sg = pslot(Tprop, P_G);
-        V q2, p2, g2;
-#pragma unroll
-        for (int s = 0; s < PPL; ++s) {
-          q2.a[s] = sq[idx(s)];
-          p2.a[s] = sp[idx(s)];
-          g2.a[s] = sg[idx(s)];
-        }
-        st(V_SMP_Q, q2);
-        st(V_SMP_P, p2);
-        st(V_SMP_G, g2);
-        Sp->smp_lp = Sp->pool_lp[Tprop];
-        Sp->smp_s2 = Sp->pool_s2[Tprop];
-      }
-    }
-    if (Tprop >= 0) used &= ~(1u << Tprop);
-    Sp->pool_used = (int)used;
-    const XF Wn = xf_add(Ww, Tw);
-    Sp->lsw_m = Wn.m;
-    Sp->lsw_e = Wn.e;
+    top_merge(q, p, g, cur_lp, cur_s2, Tw, Tprop, used, dir, d);
     const V far = ld(dir ? V_E0_P : V_E1_P), near = ld(V_PNEAR), rho = ld(V_RHO);
     V rtot, rx, ry;
 #pragma unroll
