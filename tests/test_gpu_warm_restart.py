@@ -90,3 +90,30 @@ def test_non_finite_start_fails_with_init_status(first_run):
         with pytest.raises(FitOCTError) as ei:
             pl.download()
     assert ei.value.code == -4
+
+
+def test_warm_restart_chain_addressing_across_kernels():
+    """Resumed chains keep the chain-addressing invariance: a 600-chain horseshoe plan
+    (several chains per tile, migrating kernel) resumed from a previous run's end state gives
+    chains 0..7 the same draws, bit for bit, as an 8-chain plan (one chain per tile,
+    speculative kernel) resumed from those chains' rows -- the start is read per chain
+    of the launch in every kernel variant."""
+    prob = _prob("horseshoe", 300, 8)
+    prev = sample(prob, SamplerConfig(chains=600, warmup=80, samples=10, seed=31,
+                                      max_treedepth=6))
+    cfg = SamplerConfig(chains=600, warmup=0, samples=15, seed=32, max_treedepth=6,
+                        adapt_engaged=False)
+    with Plan(prob, cfg) as pl:
+        assert pl.info["chains_per_tile"] >= 2 and pl.info["sampler"] == 1   # MIGRATE
+        pl.set_init(prev.last_q, prev.stepsize, prev.inv_metric)
+        pl.run()
+        big = pl.download()
+    small_cfg = SamplerConfig(chains=8, warmup=0, samples=15, seed=32, max_treedepth=6,
+                              adapt_engaged=False)
+    with Plan(prob, small_cfg) as pl:
+        assert pl.info["chains_per_tile"] == 1 and pl.info["sampler"] == 2   # SPECULATIVE
+        pl.set_init(prev.last_q[:8], prev.stepsize[:8], prev.inv_metric[:8])
+        pl.run()
+        small = pl.download()
+    assert np.array_equal(big.draws[:8], small.draws)
+    assert np.array_equal(big.stepsize, prev.stepsize)
