@@ -133,7 +133,8 @@ def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, adapt_delta=0.8, max_tre
     lf_rate = lf / wall
     value = draws_per_step * lf_rate / gpu_lf_per_step
     post = o["draws"][:, W:, :] if cfg.save_warmup else o["draws"]
-    return {"means": np.nanmean(post, axis=(0, 1)), "value": value, "unit": "draws/s",
+    return {"means": np.nanmean(post, axis=(0, 1)), "lf_rate": lf_rate, "value": value,
+            "unit": "draws/s",
             "cores": threads, "kind": "port",
             "value_node_est": value * hw["node_cpus"] / threads,
             "host": hw,
@@ -144,6 +145,31 @@ def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, adapt_delta=0.8, max_tre
                        f"step's {gpu_lf_per_step / draws_per_step:.1f} gradients per "
                        f"post-warmup draw; value_node_est = value x {hw['node_cpus']}/{threads}"),
             "wall_s": round(wall, 2)}
+
+
+def convergence(draws, W_saved, cols):
+    """Split and rank-normalised R-hat of the post-warmup draws over the parameter
+    columns (theta, z / yGP, the scales, sigma, br; the horseshoe's inverse-gamma
+    auxiliaries r2_* excluded), with and without the funnel-trapped chains (divergence
+    rate > 50 %), and the three worst columns by name."""
+    from fitoct_amd.stanfit import rank_rhat, split_rhat_ess
+    post = draws[:, W_saved:, :]
+    par = [j for j, n in enumerate(cols) if j >= 7 and not n.startswith("r2_")]
+    rh = {cols[j]: split_rhat_ess(post[:, :, j])[0] for j in par}
+    rrh = {cols[j]: rank_rhat(post[:, :, j]) for j in par}   # Vehtari et al. 2021
+    stuck = post[:, :, 5].mean(1) > 0.5
+    free = post[~stuck]
+    rh_free = {cols[j]: split_rhat_ess(free[:, :, j])[0] for j in par} if stuck.any() else rh
+    rrh_free = {cols[j]: rank_rhat(free[:, :, j]) for j in par} if stuck.any() else rrh
+
+    def worst(d):
+        return [[k, round(float(v), 5)] for k, v in sorted(d.items(), key=lambda t: -t[1])[:3]]
+    return {"rhat_max": round(max(rh.values()), 5), "stuck_chains": int(stuck.sum()),
+            "rhat_max_excl_stuck": round(max(rh_free.values()), 5),
+            "rank_rhat_max": round(max(rrh.values()), 5),
+            "rank_rhat_max_excl_stuck": round(max(rrh_free.values()), 5),
+            "divergent_frac": round(float(post[:, :, 5].mean()), 5),
+            "rhat_worst_columns": worst(rh), "rank_rhat_worst_columns": worst(rrh)}
 
 
 def load_traffic(workload):
@@ -173,6 +199,9 @@ def main():
                     help="0.8: rstan's default (the headline); 0.99 with --max-treedepth 12 is "
                          "the reference's hard-geometry profile (Tests/testGamma.R:45)")
     ap.add_argument("--max-treedepth", type=int, default=10)
+    ap.add_argument("--no-hard", action="store_true",
+                    help="skip the hard-geometry sub-line (one extra config-3 step at "
+                         "adapt_delta 0.99, max_treedepth 12; N = 1 only)")
     args = ap.parse_args()
     if args.config == 5 and args.iters == f"{WARMUP_IT},{SAMPLES}":
         args.iters = "%d,%d" % CONFIGS[5]["iters"]
@@ -207,7 +236,6 @@ def main():
 
     from fitoct_amd import Plan
     from fitoct_amd.api import SamplerConfig  # noqa: F401  (import check)
-    from fitoct_amd.stanfit import rank_rhat, split_rhat_ess
 
     conf = CONFIGS[args.config]
     N_bins = conf["N"]
@@ -282,13 +310,7 @@ def main():
     last = outs[-1].draws
     cols = prob.column_names()
     W_saved = outs[-1].warmup_saved
-    par = [j for j, n in enumerate(cols) if j >= 7 and not n.startswith("r2_")]
-    rh = [split_rhat_ess(last[:, W_saved:, j])[0] for j in par]
-    rrh = [rank_rhat(last[:, W_saved:, j]) for j in par]     # Vehtari et al. 2021
-    stuck = last[:, W_saved:, 5].mean(1) > 0.5       # funnel-trapped chains
-    rh_free = [split_rhat_ess(last[~stuck, W_saved:, j])[0] for j in par] if stuck.any() else rh
-    rrh_free = [rank_rhat(last[~stuck, W_saved:, j]) for j in par] if stuck.any() else rrh
-    divergent = float(last[:, W_saved:, 5].mean())
+    conv = convergence(last, W_saved, cols)
     lf_per_draw = float(np.mean(lf_steps)) / (C * (W_it + S_it))
 
     workload = (f"fitExpGP+{conf['prior']} N={N_bins} Nn={NN} {C} chains/GPU "
@@ -321,10 +343,7 @@ def main():
                    "samples": S_it, "adapt_delta": args.adapt_delta,
                    "max_treedepth": args.max_treedepth,
                    "parallelism": f"chains sharded over {world} GPU(s)"},
-        "rhat_max": round(max(rh), 5), "stuck_chains": int(stuck.sum()),
-        "rhat_max_excl_stuck": round(max(rh_free), 5),
-        "rank_rhat_max": round(max(rrh), 5), "rank_rhat_max_excl_stuck": round(max(rrh_free), 5),
-        "divergent_frac": round(divergent, 5),
+        **conv,
         "gradients_per_iteration": round(lf_per_draw, 1),
         # sampling phase alone: the kernel is gradient-bound, so its time is
         # apportioned by the post-warmup share of the last step's gradients (rank 0's chains)
@@ -347,11 +366,72 @@ def main():
         line["posterior_mean_relerr_vs_cpu"] = rel
     for pl in plans:
         pl.close()
+    if (args.config == 3 and world == 1 and not args.no_hard and args.adapt_delta == 0.8
+            and args.chains == 0 and (W_it, S_it) == (WARMUP_IT, SAMPLES)):
+        line["hard_geometry"] = hard_geometry(prob, C, local, dev, W_it, S_it, cols,
+                                              line.get("cpu_baseline"),
+                                              o_means if "cpu_baseline" in line else None)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def hard_geometry(prob, C, local, dev, W_it, S_it, cols, cpu, o_means):
+    """The north-star convergence target (max R-hat < 1.01) measured in the same run:
+    one config-3 step under the reference's own hard-geometry profile
+    (Tests/testGamma.R:45: adapt_delta 0.99, max_treedepth 12; the Shiny app's
+    'adapt_delta' / 'max_treedepth' controls, ShinyInterface/server.R:97-100), timed
+    like a headline step (inputs staged before the timer, synchronised both sides).
+    The CPU rate is the headline leg's measured oracle gradient rate scaled by this
+    step's gradients per post-warmup draw (per-gradient cost does not depend on the
+    controls), so no second CPU run is needed."""
+    import torch
+    from fitoct_amd import Plan
+    cfg = make_config(1000, C, 0, local, W_it, S_it, 0.99, 12)
+    with Plan(prob, cfg) as pl:
+        buf = torch.empty(pl.info["draws_bytes"] // 8, dtype=torch.float64, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pl.run(d_draws=buf.data_ptr(), stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        out = pl.download()
+    kms = out.kernel_ms
+    lf = out.total_leapfrogs
+    value = C * S_it / wall
+    conv = convergence(out.draws, out.warmup_saved, cols)
+    res = {"workload": (f"fitExpGP+horseshoe N={N_BINS} Nn={NN} {C} chains W={W_it} S={S_it} "
+                        "adapt_delta=0.99 max_treedepth=12 (Tests/testGamma.R:45)"),
+           "seed": 1000, "value": round(value, 2), "unit": "draws/s",
+           "ms_per_step": round(wall * 1e3, 2), "kernel_ms": round(kms, 2),
+           "gradients_per_launch": lf,
+           "gradients_per_iteration": round(lf / (C * (W_it + S_it)), 1),
+           "roofline_frac": round(f_grad(N_BINS, NN) * lf / (kms / 1e3) / 1e12
+                                  / FP64_VALU_PEAK_TF, 4),
+           **conv}
+    if cpu is not None:
+        # draws/s of the CPU path at this profile: its gradient rate over this step's
+        # gradients per post-warmup draw (warmup included, as for the GPU's value)
+        cpu_value = cpu["lf_rate"] * C * S_it / lf
+        res["cpu_baseline"] = {"value": round(cpu_value, 2), "unit": "draws/s",
+                               "cores": cpu["cores"], "kind": cpu["kind"],
+                               "value_node_est": round(cpu_value * cpu["host"]["node_cpus"]
+                                                       / cpu["cores"], 2),
+                               "sample": "the headline leg's oracle gradient rate "
+                                         f"({cpu['lf_rate']:.3g} grad/s on {cpu['cores']} "
+                                         f"threads) over this step's {lf / (C * S_it):.1f} "
+                                         "gradients per post-warmup draw"}
+        res["gpu_over_cpu"] = round(value / cpu_value, 1)
+        res["gpu_over_cpu_node_est"] = round(value / res["cpu_baseline"]["value_node_est"], 2)
+    if o_means is not None:
+        g_means = np.nanmean(out.draws[:, out.warmup_saved:, :], axis=(0, 1))
+        res["posterior_mean_relerr_vs_cpu"] = {
+            n: round(float(abs(g_means[j] - o_means[j]) / abs(o_means[j])), 6)
+            for j, n in enumerate(cols) if n.startswith("theta") or n in ("sigma", "br")}
+    return res
 
 
 def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):

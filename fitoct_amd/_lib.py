@@ -49,8 +49,11 @@ class Config(C.Structure):
         ("gamma", C.c_double), ("kappa", C.c_double), ("t0", C.c_double),
         ("init_buffer", C.c_int32), ("term_buffer", C.c_int32), ("window", C.c_int32),
         ("init_radius", C.c_double), ("save_warmup", C.c_int32), ("precision", C.c_int32),
-        ("device", C.c_int32),
+        ("device", C.c_int32), ("n_devices", C.c_int32), ("devices", C.c_int32 * 16),
     ]
+
+
+MAX_DEVICES = 16   # include/fitoct.h FITOCT_MAX_DEVICES
 
 
 class Result(C.Structure):
@@ -69,7 +72,7 @@ class PlanInfo(C.Structure):
         ("chains", C.c_int32), ("tiles", C.c_int32), ("chains_per_tile", C.c_int32),
         ("bins_per_thread", C.c_int32), ("threads_per_tile", C.c_int32),
         ("lds_bytes", C.c_int32), ("n_pad", C.c_int32), ("draws_bytes", C.c_int64),
-        ("sampler", C.c_int32), ("reserved", C.c_int32),
+        ("sampler", C.c_int32), ("n_devices", C.c_int32),
     ]
 
 
@@ -198,7 +201,7 @@ def _single_hip_runtime():
         pass
 
 
-ABI_VERSION = 3   # include/fitoct.h FITOCT_ABI_VERSION
+ABI_VERSION = 4   # include/fitoct.h FITOCT_ABI_VERSION
 
 
 def lib():

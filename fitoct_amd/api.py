@@ -131,6 +131,10 @@ class SamplerConfig:
     precision: str = "f64"
     device: int = 0
     chain_offset: int = 0
+    # device list (fitoct_config.devices): the chains are split into contiguous blocks
+    # of global chain ids, one per device, each run by its own host thread in the
+    # library; draws equal a one-device run bit for bit.  Empty: ``device`` alone.
+    devices: tuple = ()
 
     def to_c(self) -> _lib.Config:
         c = _lib.Config()
@@ -150,6 +154,12 @@ class SamplerConfig:
         c.save_warmup = 1 if self.save_warmup else 0
         c.precision = PREC[self.precision]
         c.device = int(self.device)
+        devs = tuple(int(d) for d in self.devices)
+        if len(devs) > _lib.MAX_DEVICES:
+            raise ValueError(f"at most {_lib.MAX_DEVICES} devices per call")
+        c.n_devices = len(devs)
+        for i, d in enumerate(devs):
+            c.devices[i] = d
         return c
 
 
@@ -425,8 +435,8 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
              theta0=None, Sigma0=None, lambda_rate=0.1, rho_scale=0.0, nb_warmup=500,
              nb_iter=1000, prior_PD=0, open_progress=False, *, nb_chains=4,
              prior_type="normal", lambda_scale=10.0, nu=1.0, adapt_delta=0.8,
-             max_treedepth=10, seed=None, precision="f64", device=0, refresh=1,
-             **model_switches):
+             max_treedepth=10, seed=None, precision="f64", device=0, n_gpus=None,
+             refresh=1, **model_switches):
     """Drop-in for ``FitOCTLib::fitExpGP`` (FitOCT.R:110-124).
 
     ``nb_iter`` counts warmup + sampling iterations, as the callers pass
@@ -438,6 +448,9 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
     Progress lines are printed to stdout in rstan's format whatever
     ``open_progress`` is, as the R shim does (the Shiny server parses them from its
     stdout sink, server.R:391-393,457-484); ``refresh=0`` silences them.
+    ``n_gpus`` (replaces ``options(mc.cores = detectCores())``,
+    FitOCT.R:13): the chains are split over devices ``device .. device + n_gpus - 1``
+    (the library runs one host thread per device; the draws do not depend on it).
     Returns ``dict(fit, method, xGP, prior_PD, lasso)``.
     """
     from .stanfit import StanFit
@@ -467,9 +480,10 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
                 fit.par[k] = g[k][0]
         return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,
                 "lasso": prior_type == "lasso"}
+    devices = tuple(range(int(device), int(device) + int(n_gpus))) if n_gpus and n_gpus > 1 else ()
     cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_sample, seed=seed,
                         adapt_delta=adapt_delta, max_treedepth=max_treedepth,
-                        precision=precision, device=device)
+                        precision=precision, device=device, devices=devices)
     out = sample(prob, cfg, progress=progress_printer(nb_warmup, nb_sample) if refresh else None)
     fit = StanFit.from_output(out, prob)
     return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,

@@ -42,6 +42,7 @@ SOURCES = [
     ("nuts_horseshoe", "nuts_device.hip", "hipcc", _KERNEL + ["-DFITOCT_FAMILY=2"]),
     ("nuts_monoexp", "nuts_device.hip", "hipcc", _KERNEL + ["-DFITOCT_FAMILY=3"]),
     ("fitoct_api", "fitoct_api.cpp", "hipcc", [f"--offload-arch={ARCH}", "-O2", "-std=c++17"]),
+    ("multi_device", "multi_device.cpp", "hipcc", [f"--offload-arch={ARCH}", "-O2", "-std=c++17"]),
     ("host_model", "host_model.cpp", "g++", ["-O2", "-std=c++17"]),
     ("optimize", "optimize.cpp", "g++", ["-O2", "-std=c++17"]),
     ("stan_output", "stan_output.cpp", "g++", ["-O2", "-std=c++17"]),
@@ -49,7 +50,7 @@ SOURCES = [
 # FITOCT_PROFILE=1: a diagnostic build whose kernels record cycle stamps
 # (read with FITOCT_STAMPS=1); production builds carry no timing code.
 PROFILE = os.environ.get("FITOCT_PROFILE", "0") not in ("", "0")
-HEADERS = ["kernel_params.h", "philox.h", "host_internal.h"]
+HEADERS = ["kernel_params.h", "philox.h", "host_internal.h", "plan_internal.h"]
 # FITOCT_HIPFLAGS="-DX=1 ...": extra device-compile flags for A/B variant libraries
 # (built with --force, copied aside, loaded through FITOCT_LIB_PATH)
 EXTRA = os.environ.get("FITOCT_HIPFLAGS", "").split()
@@ -77,6 +78,23 @@ def _newest_input() -> float:
     return max(os.path.getmtime(p) for p in paths)
 
 
+def _newest_dep(src: str) -> float:
+    """Newest mtime of ``src``, the headers it includes (transitively, quoted includes
+    resolved in csrc/ and include/) and this build script."""
+    import re
+    seen, todo, newest = set(), [src], os.path.getmtime(os.path.abspath(__file__))
+    while todo:
+        p = todo.pop()
+        if p in seen or not os.path.exists(p):
+            continue
+        seen.add(p)
+        newest = max(newest, os.path.getmtime(p))
+        with open(p, errors="replace") as f:
+            for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', f.read(), flags=re.M):
+                todo += [os.path.join(CSRC, inc), os.path.join(INCLUDE, inc)]
+    return newest
+
+
 def build(force: bool = False, verbose: bool = False, sanitize: bool = False) -> str:
     """Compile every translation unit and link ``fitoct_amd/libfitoct.so`` (or, with
     ``sanitize``, the ASan/UBSan host build ``fitoct_amd/build_san/libfitoct.so``)."""
@@ -95,6 +113,11 @@ def build(force: bool = False, verbose: bool = False, sanitize: bool = False) ->
     def compile_one(item):
         name, src, cc, flags = item
         obj = os.path.join(objdir, name + ".o")
+        # incremental: an object is rebuilt only if its source or a header it includes
+        # changed, or the build flags did (the sampler kernels take minutes to compile)
+        if (not force and same_flags and os.path.exists(obj)
+                and os.path.getmtime(obj) >= _newest_dep(os.path.join(CSRC, src))):
+            return obj
         if PROFILE and cc == "hipcc":
             flags = flags + ["-DFITOCT_PROFILE=1"]
         if cc == "hipcc" and EXTRA:

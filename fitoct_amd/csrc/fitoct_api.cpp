@@ -17,6 +17,7 @@
 #include "fitoct.h"
 #include "host_internal.h"
 #include "kernel_params.h"
+#include "plan_internal.h"
 
 namespace fitoct {
 hipError_t launch_family_0(bool logp, bool mixed, int bpt, int nnp, const KParams& P,
@@ -52,33 +53,6 @@ using namespace fitoct;
       return fail(FITOCT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
   } while (0)
 
-struct fitoct_plan {
-  fitoct_problem prob{};
-  fitoct_config cfg{};
-  KParams kp{};
-  int tiles = 0, bpt = 0, nnp = 15, ppl = 1, lds = 0, ncu = 0;
-  bool mixed = false;
-  int* d_mig = nullptr;       // chain-migration control block (see MigCtrl)
-  double* d_mig_img = nullptr;
-  size_t mig_bytes = 0;
-  size_t draws_bytes = 0;
-  void* d_data = nullptr;     // cx | y | isu | B  (type R)
-  double* d_draws = nullptr;  // internal draws buffer (lazily allocated)
-  double* d_stack = nullptr;
-  double* d_fin = nullptr;    // eps[C] | minv[C*D] | q[C*D]
-  double* d_init = nullptr;   // warm restart (fitoct_plan_set_init): eps[C] | minv[C*D] | q[C*D]
-  int* d_status = nullptr;
-  long long* d_leap = nullptr;
-  KParams* d_kp = nullptr;    // device copy of the launch parameters
-  double* last_draws = nullptr;
-  double kernel_ms = 0.0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool ran = false;
-  bool launched = false;      // fitoct_plan_launch issued, fitoct_plan_wait not yet
-  int* h_prog = nullptr;      // host-pinned [chains]: transitions done (kernel-written)
-  int* h_cancel = nullptr;    // host-pinned flag polled by the kernel
-  long long* d_stamps = nullptr;   // diagnostic stamps of the launch in flight
-};
 
 struct fitoct_evaluator {
   fitoct_plan* pl = nullptr;
@@ -440,6 +414,7 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
 
 void free_plan(fitoct_plan* pl) {
   if (!pl) return;
+  for (fitoct_plan* sh : pl->shards) free_plan(sh);
   (void)hipFree(pl->d_data);
   (void)hipFree(pl->d_draws);
   (void)hipFree(pl->d_stack);
@@ -653,7 +628,18 @@ int32_t fitoct_logp_grad(const fitoct_problem* prob, int32_t n_points, const dou
 int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
                            fitoct_plan** out) {
   return guarded(__func__, [&]() -> int32_t {
-    return plan_create(prob, cfg, 0, -1, out);
+    if (!out) return fail(FITOCT_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (!cfg) return fail(FITOCT_E_ARG, "config is NULL");
+    if (cfg->chains < 1) return fail(FITOCT_E_ARG, "chains must be >= 1");
+    std::vector<int> devs;
+    const int rc = resolve_devices(cfg, cfg->chains, devs);
+    if (rc) return rc;
+    if (devs.size() > 1) return group_plan_create(prob, cfg, devs, out);
+    fitoct_config c = *cfg;
+    c.device = devs[0];
+    c.n_devices = 0;
+    return plan_create(prob, &c, 0, -1, out);
   });
 }
 
@@ -777,6 +763,7 @@ extern "C" {
 int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
   return guarded(__func__, [&]() -> int32_t {
     if (!pl || !info) return fail(FITOCT_E_ARG, "NULL argument");
+    if (!pl->shards.empty()) return group_plan_info(pl, info);
     info->dim = pl->kp.D;
     info->n_cols = pl->kp.ncols;
     info->iters_saved = pl->kp.iters_saved;
@@ -785,7 +772,7 @@ int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
     info->chains_per_tile = pl->kp.G;
     info->sampler = pl->mig_bytes > 0 ? FITOCT_SAMPLER_MIGRATE
                     : pl->kp.spec ? FITOCT_SAMPLER_SPECULATIVE : FITOCT_SAMPLER_PLAIN;
-    info->reserved = 0;
+    info->n_devices = 1;
     info->bins_per_thread = pl->bpt;
     info->threads_per_tile = TPB;
     info->lds_bytes = pl->lds;
@@ -799,6 +786,7 @@ int32_t fitoct_plan_set_init(fitoct_plan* pl, const double* q_init, const double
                              const double* inv_metric) {
   return guarded(__func__, [&]() -> int32_t {
     if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    if (!pl->shards.empty()) return group_plan_set_init(pl, q_init, stepsize, inv_metric);
     if (pl->launched) return fail(FITOCT_E_ARG, "plan is running: call fitoct_plan_wait first");
     const int C = pl->kp.chains, D = pl->kp.D;
     // checked on the host: the kernel takes every value as given
@@ -833,6 +821,7 @@ int32_t fitoct_plan_set_init(fitoct_plan* pl, const double* q_init, const double
 int32_t fitoct_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
   return guarded(__func__, [&]() -> int32_t {
     if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    if (!pl->shards.empty()) return group_plan_launch(pl, d_draws, stream);
     if (pl->launched) return fail(FITOCT_E_ARG, "plan is running: call fitoct_plan_wait first");
     HIP_TRY(hipSetDevice(pl->cfg.device));
     if (pl->h_prog) {   // no launch of this plan is in flight: the kernel does not touch them
@@ -872,6 +861,7 @@ int32_t fitoct_plan_poll(fitoct_plan* pl, int64_t* iterations_done, int64_t* ite
                          int32_t* finished) {
   return guarded(__func__, [&]() -> int32_t {
     if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    if (!pl->shards.empty()) return group_plan_poll(pl, iterations_done, iterations_total, finished);
     const int C = pl->kp.chains;
     int64_t done = 0;
     if (pl->h_prog)
@@ -894,6 +884,7 @@ int32_t fitoct_plan_poll(fitoct_plan* pl, int64_t* iterations_done, int64_t* ite
 int32_t fitoct_plan_cancel(fitoct_plan* pl) {
   return guarded(__func__, [&]() -> int32_t {
     if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    if (!pl->shards.empty()) return group_plan_cancel(pl);
     if (!pl->h_cancel) return fail(FITOCT_E_ARG, "this plan has no cancellation flag (batch plan)");
     __atomic_store_n(pl->h_cancel, 1, __ATOMIC_SEQ_CST);
     return FITOCT_OK;
@@ -903,6 +894,7 @@ int32_t fitoct_plan_cancel(fitoct_plan* pl) {
 int32_t fitoct_plan_wait(fitoct_plan* pl) {
   return guarded(__func__, [&]() -> int32_t {
     if (!pl) return fail(FITOCT_E_ARG, "plan is NULL");
+    if (!pl->shards.empty()) return group_plan_wait(pl);
     if (!pl->launched) return pl->ran ? FITOCT_OK : fail(FITOCT_E_ARG, "plan has not been launched");
     HIP_TRY(hipSetDevice(pl->cfg.device));
     pl->launched = false;
@@ -1013,6 +1005,7 @@ int32_t fitoct_plan_run(fitoct_plan* pl, void* d_draws, void* stream) {
 int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
   return guarded(__func__, [&]() -> int32_t {
     if (!pl || !res) return fail(FITOCT_E_ARG, "NULL argument");
+    if (!pl->shards.empty()) return group_plan_download(pl, res);
     if (!pl->ran) return fail(FITOCT_E_ARG, "plan has not run");
     HIP_TRY(hipSetDevice(pl->cfg.device));
     const KParams& k = pl->kp;
@@ -1041,11 +1034,16 @@ int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
     long long tot = 0;
     for (long long v : lf) tot += v;
     res->total_leapfrogs = tot;
-    for (int c = 0; c < C; ++c)
-      if (st[c] != 0) {
-        return fail(st[c], "chain " + std::to_string(k.chain_offset + c) + " failed with status " +
-                               std::to_string(st[c]));
-      }
+    // a chain's own failure is reported before the cancellations it may have caused
+    // (a multi-device plan cancels the other devices' chains when one fails)
+    int bad = -1;
+    for (int c = 0; c < C && bad < 0; ++c)
+      if (st[c] != 0 && st[c] != FITOCT_E_CANCELLED) bad = c;
+    for (int c = 0; c < C && bad < 0; ++c)
+      if (st[c] != 0) bad = c;
+    if (bad >= 0)
+      return fail(st[bad], "chain " + std::to_string(k.chain_offset + bad) + " failed with status " +
+                               std::to_string(st[bad]));
     return FITOCT_OK;
   });
 }
@@ -1056,6 +1054,18 @@ int32_t fitoct_expgp_sample(const fitoct_problem* prob, const fitoct_config* cfg
                             fitoct_result* res) {
   return guarded(__func__, [&]() -> int32_t {
     const auto t0 = std::chrono::steady_clock::now();
+    if (cfg && cfg->chains >= 1) {   // several devices: one host thread per device
+      std::vector<int> devs;
+      const int rd = resolve_devices(cfg, cfg->chains, devs);
+      if (rd) return rd;
+      if (devs.size() > 1) {
+        const int rg = group_sample(prob, cfg, devs, res);
+        if (res)
+          res->wall_ms = std::chrono::duration<double, std::milli>(
+                             std::chrono::steady_clock::now() - t0).count();
+        return rg;
+      }
+    }
     fitoct_plan* pl = nullptr;
     int rc = fitoct_plan_create(prob, cfg, &pl);
     if (rc) return rc;
@@ -1095,22 +1105,11 @@ int32_t fitoct_rank_rhat(const double* x, int32_t chains, int32_t n, double* rha
 // global chain cfg.chain_offset + p*chains + c: its draws are those of a single
 // plan of that problem with chain_offset = cfg.chain_offset + p*chains.
 // ---------------------------------------------------------------------------
-struct fitoct_batch {
-  std::vector<fitoct_plan*> plans;
-  fitoct_config cfg{};
-  int tiles = 0;
-  size_t per_bytes = 0;       // draws bytes of one problem
-  KParams* d_kp = nullptr;    // [n_problems]
-  int* d_map = nullptr;       // [tiles][2]
-  double* d_draws = nullptr;  // internal [n_problems][chains][iters][cols] (lazy)
-  double kernel_ms = 0.0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool ran = false;
-};
 
 namespace {
 void free_batch(fitoct_batch* b) {
   if (!b) return;
+  for (fitoct_batch* sb : b->subs) free_batch(sb);
   for (fitoct_plan* pl : b->plans) free_plan(pl);
   (void)hipFree(b->d_kp);
   (void)hipFree(b->d_map);
@@ -1133,16 +1132,25 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
     if (cfg->chains < 1) return fail(FITOCT_E_ARG, "chains must be >= 1");
     if ((int64_t)n_problems * cfg->chains > (int64_t)1 << 30)
       return fail(FITOCT_E_ARG, "too many chains in one batch");
+    std::vector<int> devs;
+    {
+      const int rd = resolve_devices(cfg, n_problems, devs);
+      if (rd) return rd;
+    }
+    if (devs.size() > 1) return group_batch_create(probs, n_problems, cfg, devs, out);
     std::unique_ptr<fitoct_batch, void (*)(fitoct_batch*)> guard(new fitoct_batch(), free_batch);
     fitoct_batch* b = guard.get();
     b->cfg = *cfg;
+    b->cfg.device = devs[0];
+    b->cfg.n_devices = 0;
+    b->n_problems = n_problems;
     const int C = cfg->chains;
     auto build = [&]() -> int {
       for (int p = 0; p < n_problems; ++p) {
         if (probs[p].prior_type != probs[0].prior_type || probs[p].Nn != probs[0].Nn)
           return fail(FITOCT_E_ARG, "batch problems must share prior_type and Nn (problem " +
                                         std::to_string(p) + ")");
-        fitoct_config c = *cfg;
+        fitoct_config c = b->cfg;
         c.chain_offset = cfg->chain_offset + p * C;
         fitoct_plan* pl = nullptr;
         const int rc = plan_create(&probs[p], &c, n_problems * C, -1, &pl);
@@ -1165,7 +1173,7 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
         for (size_t p = 0; p < b->plans.size(); ++p) {
           fitoct_plan* pl = b->plans[p];
           if (pl && pl->bpt == to) continue;
-          fitoct_config c = *cfg;
+          fitoct_config c = b->cfg;
           c.chain_offset = cfg->chain_offset + (int)p * C;
           free_plan(pl);
           b->plans[p] = nullptr;
@@ -1187,7 +1195,7 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
           map.push_back(c0);
         }
       b->tiles = (int)map.size() / 2;
-      HIP_TRY(hipSetDevice(cfg->device));
+      HIP_TRY(hipSetDevice(b->cfg.device));
       HIP_TRY(hipMalloc(&b->d_map, sizeof(int) * map.size()));
       HIP_TRY(hipMemcpy(b->d_map, map.data(), sizeof(int) * map.size(), hipMemcpyHostToDevice));
       HIP_TRY(hipMalloc(&b->d_kp, sizeof(KParams) * n_problems));
@@ -1205,6 +1213,7 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
 int32_t fitoct_batch_get_info(const fitoct_batch* b, fitoct_plan_info* info) {
   return guarded(__func__, [&]() -> int32_t {
     if (!b || !info) return fail(FITOCT_E_ARG, "NULL argument");
+    if (!b->subs.empty()) return group_batch_info(b, info);
     const int rc = fitoct_plan_get_info(b->plans[0], info);
     if (rc) return rc;
     info->chains = b->cfg.chains * (int)b->plans.size();
@@ -1217,6 +1226,7 @@ int32_t fitoct_batch_get_info(const fitoct_batch* b, fitoct_plan_info* info) {
 int32_t fitoct_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
   return guarded(__func__, [&]() -> int32_t {
     if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
+    if (!b->subs.empty()) return group_batch_run(b, d_draws, stream);
     HIP_TRY(hipSetDevice(b->cfg.device));
     const size_t P = b->plans.size();
     double* dst = (double*)d_draws;
@@ -1254,8 +1264,9 @@ int32_t fitoct_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
 int32_t fitoct_batch_download(fitoct_batch* b, int32_t problem, fitoct_result* res) {
   return guarded(__func__, [&]() -> int32_t {
     if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
-    if (problem < 0 || problem >= (int32_t)b->plans.size())
+    if (problem < 0 || problem >= b->n_problems)
       return fail(FITOCT_E_ARG, "problem index out of range");
+    if (!b->subs.empty()) return group_batch_download(b, problem, res);
     if (!b->ran) return fail(FITOCT_E_ARG, "batch has not run");
     return fitoct_plan_download(b->plans[problem], res);
   });

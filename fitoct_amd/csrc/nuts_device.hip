@@ -313,6 +313,10 @@ __device__ __forceinline__ XF xf_norm(double m, int e) {
 }
 __device__ __forceinline__ XF xf_exp(double x) {   // exp(x), x <= +inf; -inf -> 0
   if (x > -700.0 && x < 700.0) return xf_norm(fexp(x), 0);
+  // above 1e8 (an energy drop no trajectory of a finite start reaches) the weight
+  // saturates: the exponent stays within int, and so does the exponent difference of
+  // two weights in xf_u_below (>= -1.45e9 - 1.45e8)
+  if (!(x < 1.0e8)) x = 1.0e8;
   // below -1e9 (a divergent leaf: its weight is never merged) the exponent would not fit
   // an int; the weight is 0 to every digit the merges can resolve
   if (!(x > -1.0e9)) return XF{0.0, 0};
@@ -2361,11 +2365,19 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       Ch ch(P, L, 0, c0, lane, nct);
       int seen = 0;
       long long spins = 0;
+      unsigned long long t_idle = 0;
       for (;;) {
         const int r = lds_load(&help_req);
         if (r < 0) break;                       // the chain has finished
         if (r == seen) {
-          if (++spins > SPIN_LIMIT) break;
+          // the chain releases its helper when it finishes (help_req = -1), however long
+          // its gaps between speculated leaves (init, step-size searches): the hang guard
+          // is in real time, not polls, as for migration receivers
+          if (++spins > SPIN_LIMIT) {
+            if (spins == SPIN_LIMIT + 1) t_idle = __builtin_amdgcn_s_memrealtime();
+            if (__builtin_amdgcn_s_memrealtime() - t_idle > MIG_WAIT_TICKS) break;
+            __builtin_amdgcn_s_sleep(32);
+          }
           __builtin_amdgcn_s_sleep(1);
           continue;
         }

@@ -48,9 +48,11 @@ def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=N
     return their local output without draws.
 
     ``resume`` (warm restart, :meth:`fitoct_amd.api.Plan.set_init`): a previous run of
-    the same global chains (e.g. this function's rank-0 output, available on every
-    rank); each rank starts its block from that run's last positions, step sizes and
-    inverse metrics.  With ``engine`` they reach it as ``engine(prob, cfg, init=(q,
+    the same global chains -- the full output with every chain, e.g. this function's
+    rank-0 output, which the caller must make available on every rank (broadcast it:
+    non-zero ranks only get their local block back) -- with the same ``chain_offset``;
+    each rank starts its block from that run's last positions, step sizes and inverse
+    metrics.  With ``engine`` they reach it as ``engine(prob, cfg, init=(q,
     stepsize, inv_metric))``.
 
     Without ``engine`` each rank's HIP plan writes its draws into a device tensor;
@@ -71,7 +73,12 @@ def sample_sharded(prob: ExpGPProblem, cfg: SamplerConfig, engine=None, device=N
     init = None
     if resume is not None:
         if len(resume.stepsize) != cfg.chains or resume.last_q.shape != (cfg.chains, prob.D):
-            raise ValueError("resume must hold the cfg.chains chains of a previous run")
+            raise ValueError("resume must hold the cfg.chains chains of a previous run "
+                             "(rank 0's full output, broadcast to every rank)")
+        if resume.chain_offset != cfg.chain_offset:
+            raise ValueError(f"resume holds global chains from {resume.chain_offset}, this run "
+                             f"starts at {cfg.chain_offset}: chains would be paired with others' "
+                             "positions")
         blk = slice(offset, offset + count)
         init = (resume.last_q[blk], resume.stepsize[blk], resume.inv_metric[blk])
     nccl = dist.get_backend() == "nccl"

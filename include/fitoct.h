@@ -34,9 +34,11 @@
 extern "C" {
 #endif
 
-#define FITOCT_ABI_VERSION 3
+#define FITOCT_ABI_VERSION 4
 /* largest accepted N (depth bins): bounds every host and device allocation derived from it */
 #define FITOCT_MAX_BINS (1 << 22)
+/* largest device list of one call (fitoct_config.devices) */
+#define FITOCT_MAX_DEVICES 16
 
 typedef enum fitoct_status {
   FITOCT_OK = 0,
@@ -103,7 +105,19 @@ typedef struct fitoct_config {
   double init_radius;    /* jitter around the default init (0 -> deterministic) */
   int32_t save_warmup;   /* 1: warmup draws are stored too (traceplot(inc_warmup=TRUE)) */
   int32_t precision;     /* FITOCT_PREC_* */
-  int32_t device;        /* HIP device ordinal */
+  int32_t device;        /* HIP device ordinal (used when n_devices == 0) */
+  /* Device list (SURVEY.md §8b "device list"; R fitExpGP(n_gpus = k) passes 0..k-1).  This
+   * replaces rstan's chain parallelism over host cores, options(mc.cores =
+   * parallel::detectCores()) at FitOCT.R:13 / ShinyInterface/server.R:19.  With
+   * n_devices >= 1 the call's chains are split into contiguous blocks of global chain ids,
+   * block r = [chain_offset + off_r, chain_offset + off_r + count_r) with count_r =
+   * chains / n + (r < chains % n) and off_r = r * (chains / n) + min(r, chains % n), run
+   * on devices[r] by one host thread per device (a batch splits its problems the same
+   * way).  Random streams are keyed by global chain id, so the draws are bit-identical
+   * to a one-device run whatever the list.  Only the first min(n_devices, chains) entries
+   * (problems, for a batch) are used; an ordinal may repeat (several plans on one GPU). */
+  int32_t n_devices;     /* 0: `device` alone; 1..FITOCT_MAX_DEVICES */
+  int32_t devices[FITOCT_MAX_DEVICES];
 } fitoct_config;
 
 /* Outputs; every pointer is caller-allocated (NULL = not wanted). */
@@ -137,7 +151,7 @@ typedef struct fitoct_plan_info {
   int32_t n_pad;           /* padded bin count */
   int64_t draws_bytes;     /* size of the draws buffer */
   int32_t sampler;         /* sampler variant launched: FITOCT_SAMPLER_* */
-  int32_t reserved;
+  int32_t n_devices;       /* devices the plan's chains (a batch's problems) run on */
 } fitoct_plan_info;
 
 /* fitoct_plan_info::sampler.  PLAIN: tiles of several chains, or migration off;
@@ -197,7 +211,13 @@ int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
 int32_t fitoct_plan_get_info(const fitoct_plan* plan, fitoct_plan_info* info);
 /* Run the sampler on `stream` (hipStream_t; NULL = default stream).  If d_draws is
  * non-NULL the draws go to that caller-owned DEVICE buffer (>= info.draws_bytes),
- * otherwise to a plan-internal one.  Returns after the kernel completes. */
+ * otherwise to a plan-internal one.  Returns after the kernel completes.
+ * Multi-device plans (cfg.n_devices > 1): `stream` must be NULL (each device runs on
+ * its default stream); d_draws may live on any device: the shards on that device write
+ * their blocks in place and every other block is copied into it peer-to-peer over xGMI
+ * once its device has finished (the one gather of SURVEY.md §8e, inside one process).
+ * The poll / cancel / wait / download / set_init calls below act on every device; a
+ * failure on one device cancels the others and the call returns that one status. */
 int32_t fitoct_plan_run(fitoct_plan* plan, void* d_draws, void* stream);
 /* The same run in two halves, for long fits driven from an interactive host.  It
  * replaces the progress that rstan writes to stan.log and the Shiny server reads

@@ -394,6 +394,10 @@ static xf xf_norm(double m, int e) {
 }
 static xf xf_exp(double x) {
   if (x > -700.0 && x < 700.0) return xf_norm(exp(x), 0);
+  /* above 1e8 (an energy drop no trajectory of a finite start reaches) the weight
+   * saturates: the exponent stays within int and exponent differences of two weights
+   * (xf_u_below) stay within int too (>= -1.45e9 - 1.45e8) */
+  if (!(x < 1.0e8)) x = 1.0e8;
   /* below -1e9 (a divergent leaf, never merged) the exponent would overflow an int
    * (UBSan, scripts/cpu_sanitized_suite.sh); the weight is 0 to every resolvable digit */
   if (!(x > -1.0e9)) {
@@ -626,20 +630,18 @@ static int init_stepsize(nuts_ctx* c, ps_point* z, uint32_t window, double* eps)
   return rc;
 }
 
-/* warm restart (oracle_set_init, the restatement of fitoct_plan_set_init): per-chain
- * initial step size [chains], inverse metric [chains][D] and position [chains][D] of the
- * next oracle_sample calls; NULL = the defaults below.  Caller-owned, read-only. */
-static const double *g_init_eps, *g_init_minv, *g_init_q;
-
-void oracle_set_init(const double* q_init, const double* stepsize, const double* inv_metric) {
-  g_init_q = q_init;
-  g_init_eps = stepsize;
-  g_init_minv = inv_metric;
-}
+/* warm restart (oracle_sample_init, the restatement of fitoct_plan_set_init): per-chain
+ * initial position [chains][D], step size [chains] and inverse metric [chains][D];
+ * NULL = the defaults below.  Caller-owned, read-only, passed per call (no global state:
+ * concurrent oracle_sample calls from several host threads are independent). */
+typedef struct {
+  const double *q, *eps, *minv;
+} warm_init;
 
 /* one chain: init, adaptation (adapt_diag_e_nuts), sampling */
-static int run_chain(const model* m, const fitoct_config* cfg, int lc, double* draws, int ncols,
-                     int iters_saved, double* out_eps, double* out_minv, long long* out_lf) {
+static int run_chain(const model* m, const fitoct_config* cfg, const warm_init* wi, int lc,
+                     double* draws, int ncols, int iters_saved, double* out_eps, double* out_minv,
+                     long long* out_lf) {
   const int D = m->D, Nn = m->Nn, W = cfg->warmup, S = cfg->samples;
   const uint32_t gid = (uint32_t)(cfg->chain_offset + lc);
   nuts_ctx c;
@@ -650,7 +652,7 @@ static int run_chain(const model* m, const fitoct_config* cfg, int lc, double* d
   c.minv = (double*)malloc(sizeof(double) * D);
   c.work = (double*)malloc(sizeof(double) * 3 * (Nn + 1));
   pt_alloc(&c.z, D);
-  for (int k = 0; k < D; ++k) c.minv[k] = g_init_minv ? g_init_minv[(size_t)lc * D + k] : 1.0;
+  for (int k = 0; k < D; ++k) c.minv[k] = wi->minv ? wi->minv[(size_t)lc * D + k] : 1.0;
   ps_point z;
   pt_alloc(&z, D);
   /* initial point: jitter around theta0 (inits) */
@@ -668,18 +670,18 @@ static int run_chain(const model* m, const fitoct_config* cfg, int lc, double* d
         if (m->fam == 0 && k == 3 + Nn) base = -log(m->rate);
       }
       z.q[k] = base + cfg->init_radius * w * (2.0 * unif(c.key, (uint32_t)attempt, T_INIT, (uint32_t)k, 0u) - 1.0);
-      if (g_init_q) z.q[k] = g_init_q[(size_t)lc * D + k];
+      if (wi->q) z.q[k] = wi->q[(size_t)lc * D + k];
     }
     z.lp = logp_grad(m, z.q, z.g, &z.s2, c.work);
     int finite = z.lp > -INFINITY;
     for (int k = 0; k < D; ++k) finite = finite && isfinite(z.g[k]);
     if (finite) break;
-    if (attempt + 1 >= 100 || g_init_q) { /* a given start is not retried */
+    if (attempt + 1 >= 100 || wi->q) { /* a given start is not retried */
       rc = FITOCT_E_INIT;
       break;
     }
   }
-  double eps = g_init_eps ? g_init_eps[lc] : cfg->stepsize;
+  double eps = wi->eps ? wi->eps[lc] : cfg->stepsize;
   /* dual averaging */
   double mu = log(10 * eps), s_bar = 0, x_bar = 0;
   int da_n = 0;
@@ -807,9 +809,12 @@ void oracle_normals(uint64_t seed, uint32_t stream, uint32_t tag, uint32_t it, u
   }
 }
 
-/* draws: [chains][iters_saved][D + 8] (same columns as libfitoct) */
-int oracle_sample(const fitoct_problem* p, const fitoct_config* cfg, double* draws,
-                  double* stepsize, double* inv_metric, long long* leapfrogs, int nthreads) {
+/* draws: [chains][iters_saved][D + 8] (same columns as libfitoct); q_init / init_eps /
+ * init_minv: the warm restart above (each may be NULL) */
+int oracle_sample_init(const fitoct_problem* p, const fitoct_config* cfg, double* draws,
+                       double* stepsize, double* inv_metric, long long* leapfrogs, int nthreads,
+                       const double* q_init, const double* init_eps, const double* init_minv) {
+  const warm_init wi = {q_init, init_eps, init_minv};
   model m;
   if (model_init(&m, p)) return -1;
   const int ncols = m.D + 8;
@@ -820,10 +825,17 @@ int oracle_sample(const fitoct_problem* p, const fitoct_config* cfg, double* dra
 #pragma omp parallel for schedule(dynamic, 1) reduction(min : rc_all)
 #endif
   for (int lc = 0; lc < cfg->chains; ++lc) {
-    const int rc = run_chain(&m, cfg, lc, draws, ncols, iters_saved, stepsize, inv_metric, leapfrogs);
+    const int rc =
+        run_chain(&m, cfg, &wi, lc, draws, ncols, iters_saved, stepsize, inv_metric, leapfrogs);
     if (rc < rc_all) rc_all = rc;
   }
   (void)nthreads;
   free(m.B);
   return rc_all;
+}
+
+int oracle_sample(const fitoct_problem* p, const fitoct_config* cfg, double* draws,
+                  double* stepsize, double* inv_metric, long long* leapfrogs, int nthreads) {
+  return oracle_sample_init(p, cfg, draws, stepsize, inv_metric, leapfrogs, nthreads, NULL, NULL,
+                            NULL);
 }

@@ -48,8 +48,8 @@ def lib():
                                     C.POINTER(C.c_uint32)]
         L.oracle_normals.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_int, dp]
-        L.oracle_set_init.argtypes = [dp, dp, dp]
-        L.oracle_set_init.restype = None
+        L.oracle_sample_init.argtypes = [C.POINTER(abi.Problem), C.POINTER(abi.Config), dp, dp,
+                                         dp, C.POINTER(C.c_longlong), C.c_int, dp, dp, dp]
         _L = L
     return _L
 
@@ -102,12 +102,9 @@ def sample(prob, cfg, nthreads: int = 0, q_init=None, init_stepsize=None, init_i
     minv = np.zeros((cfg.chains, D))
     lf = np.zeros(cfg.chains, dtype=np.int64)
     p, c = prob.to_c(), cfg.to_c()
-    lib().oracle_set_init(*[None if a is None else _dp(a) for a in arrs])
-    try:
-        rc = lib().oracle_sample(C.byref(p), C.byref(c), _dp(draws), _dp(eps), _dp(minv),
-                                 lf.ctypes.data_as(C.POINTER(C.c_longlong)), int(nthreads))
-    finally:
-        lib().oracle_set_init(None, None, None)
+    rc = lib().oracle_sample_init(C.byref(p), C.byref(c), _dp(draws), _dp(eps), _dp(minv),
+                                  lf.ctypes.data_as(C.POINTER(C.c_longlong)), int(nthreads),
+                                  *[None if a is None else _dp(a) for a in arrs])
     if rc != 0:
         raise RuntimeError(f"oracle_sample failed with status {rc}")
     return {"draws": draws, "stepsize": eps, "inv_metric": minv, "leapfrogs": lf}

@@ -9,6 +9,13 @@
 
 fitoct_device_count <- function() .Call(fitoct_R_device_count)
 
+# n_gpus GPUs from `device` on (n_gpus = NA: every visible GPU from `device` on)
+fitoct_devices <- function(device, n_gpus) {
+  if (is.na(n_gpus)) n_gpus <- max(1L, fitoct_device_count() - as.integer(device))
+  if (n_gpus < 1 || n_gpus > 16) stop('fitExpGP: n_gpus must be in 1..16')
+  as.integer(device) + seq_len(as.integer(n_gpus)) - 1L
+}
+
 # GP control grid (server.R:623-631)
 fitoct_xGP <- function(Nn, gridType) {
   if (gridType == 'internal') {
@@ -30,15 +37,17 @@ fitoct_problem <- function(x, y, uy, dataType, Nn, gridType, rho_scale, theta0, 
 
 # sampling: stdout gets rstan-format "Chain k: Iteration: ..." lines (the Shiny server
 # parses them from its stan.log sink, server.R:391-393,457-484)
+# devices: GPU ordinals; the library splits the chains over them (one host thread per
+# GPU), which replaces options(mc.cores = parallel::detectCores()) (FitOCT.R:13, server.R:19)
 fitoct_sample <- function(prob, nb_chains, nb_warmup, nb_iter, seed, adapt_delta,
-                          max_treedepth, device) {
+                          max_treedepth, devices) {
   files <- vapply(seq_len(nb_chains), function(i) tempfile(fileext = '.csv'), character(1))
   on.exit(unlink(files))
   .Call(fitoct_R_sample, prob,
         list(chains = as.integer(nb_chains), warmup = as.integer(nb_warmup),
              samples = as.integer(nb_iter - nb_warmup), seed = as.double(seed),
              adapt_delta = as.double(adapt_delta), max_treedepth = as.integer(max_treedepth),
-             device = as.integer(device)),
+             devices = as.integer(devices)),
         files)
   rstan::read_stan_csv(files)
 }
@@ -71,9 +80,10 @@ fitExpGP <- function(x, y, uy, dataType = 2, Nn = 10, gridType = 'internal',
                      prior_type = c('normal', 'lasso', 'horseshoe'),
                      lambda_scale = 10, nu = 1, adapt_delta = 0.8, max_treedepth = 10,
                      seed = sample.int(.Machine$integer.max, 1),
-                     backend = c('hip', 'rstan'), device = 0L) {
+                     backend = c('hip', 'rstan'), device = 0L, n_gpus = 1L) {
   backend <- match.arg(backend)
   prior_type <- match.arg(prior_type)
+  devices <- fitoct_devices(device, n_gpus)
   if (backend == 'rstan')
     return(FitOCTLib::fitExpGP(x = x, y = y, uy = uy, dataType = dataType, Nn = Nn,
                                gridType = gridType, method = method, theta0 = theta0,
@@ -86,7 +96,7 @@ fitExpGP <- function(x, y, uy, dataType = 2, Nn = 10, gridType = 'internal',
                          lambda_rate, lambda_scale, nu, prior_PD)
   fit <- switch(method,
     sample = fitoct_sample(prob, nb_chains, nb_warmup, nb_iter, seed, adapt_delta,
-                           max_treedepth, device),
+                           max_treedepth, devices),
     optim = fitoct_optimize(prob, device),
     vb = fitoct_vb(prob, seed, device),
     stop("fitExpGP: method must be 'sample', 'optim' or 'vb'"))
@@ -100,14 +110,15 @@ fitExpGP <- function(x, y, uy, dataType = 2, Nn = 10, gridType = 'internal',
 fitMonoExp <- function(x, y, uy, dataType = 2, method = 'optim', nb_warmup = 500,
                        nb_iter = 1500, nb_chains = 4,
                        seed = sample.int(.Machine$integer.max, 1),
-                       backend = c('hip', 'rstan'), device = 0L) {
+                       backend = c('hip', 'rstan'), device = 0L, n_gpus = 1L) {
   backend <- match.arg(backend)
+  devices <- fitoct_devices(device, n_gpus)
   if (backend == 'rstan')
     return(FitOCTLib::fitMonoExp(x = x, y = y, uy = uy, dataType = dataType))
   theta0 <- .Call(fitoct_R_mono_theta0, as.double(x), as.double(y), as.integer(dataType))
   prob <- fitoct_problem(x, y, uy, dataType, 2L, 'extremal', 0, theta0, diag(3), 3L)
   if (method == 'sample') {
-    fit <- fitoct_sample(prob, nb_chains, nb_warmup, nb_iter, seed, 0.8, 10, device)
+    fit <- fitoct_sample(prob, nb_chains, nb_warmup, nb_iter, seed, 0.8, 10, devices)
     th <- as.matrix(fit, pars = 'theta')
     return(list(fit = fit, method = method, best.theta = colMeans(th), cor.theta = cor(th)))
   }

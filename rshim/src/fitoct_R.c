@@ -89,7 +89,10 @@ static void stop_on(int32_t rc) {
 }
 
 /* .Call(fitoct_R_sample, prob, ctrl, files): ctrl = list(chains, warmup, samples, seed,
- * adapt_delta, max_treedepth, device); one Stan CSV per chain at files[] */
+ * adapt_delta, max_treedepth, devices); one Stan CSV per chain at files[].  devices: the
+ * integer device list (fitExpGP(n_gpus = k, device = d) passes d, ..., d + k - 1): the
+ * library splits the chains into contiguous blocks, one host thread per GPU, and still
+ * returns only on the R main thread (SURVEY.md §8b threading) */
 SEXP fitoct_R_sample(SEXP prob, SEXP ctrl, SEXP files) {
   fitoct_problem p;
   fitoct_config c;
@@ -101,7 +104,13 @@ SEXP fitoct_R_sample(SEXP prob, SEXP ctrl, SEXP files) {
   c.seed = (uint64_t)num(ctrl, "seed");
   c.adapt_delta = num(ctrl, "adapt_delta");
   c.max_treedepth = inum(ctrl, "max_treedepth");
-  c.device = inum(ctrl, "device");
+  SEXP devs = elt(ctrl, "devices");
+  if (TYPEOF(devs) != INTSXP || XLENGTH(devs) < 1 || XLENGTH(devs) > FITOCT_MAX_DEVICES)
+    Rf_error("fitoct: devices must be an integer vector of 1 to %d device ordinals",
+             FITOCT_MAX_DEVICES);
+  c.device = INTEGER(devs)[0];
+  c.n_devices = (int32_t)XLENGTH(devs);
+  for (int i = 0; i < c.n_devices; ++i) c.devices[i] = INTEGER(devs)[i];
   if (TYPEOF(files) != STRSXP || XLENGTH(files) != c.chains)
     Rf_error("fitoct: one output file per chain is required");
   const char** paths = (const char**)R_alloc((size_t)c.chains, sizeof(char*));

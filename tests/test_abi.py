@@ -46,7 +46,7 @@ def test_struct_layouts_match_ctypes():
     sizes = _lib.struct_sizes()
     assert sizes == (C.sizeof(_lib.Problem), C.sizeof(_lib.Config), C.sizeof(_lib.Result),
                      C.sizeof(_lib.PlanInfo))
-    assert _lib.lib().fitoct_abi_version() == 3
+    assert _lib.lib().fitoct_abi_version() == 4 == _lib.ABI_VERSION
 
 
 def test_default_config_is_stan_default():
@@ -223,3 +223,57 @@ def test_set_init_needs_a_plan():
     L = _lib.lib()
     assert L.fitoct_plan_set_init(None, None, None, None) == -1
     assert b"plan" in L.fitoct_last_error()
+
+
+def _tiny_problem():
+    x = np.linspace(20, 500, 16)
+    return ExpGPProblem(x, x * 0 + 1000, x * 0 + 1.0, Nn=5)
+
+
+@pytest.mark.parametrize("devices,n_override,msg", [
+    ((0,) * 17, None, "n_devices"),          # more than FITOCT_MAX_DEVICES
+    ((0, -1), None, "negative"),             # a negative ordinal
+    ((0, 1), -2, "n_devices"),               # n_devices < 0
+])
+def test_device_list_argument_errors(devices, n_override, msg):
+    """fitoct_config.devices (SURVEY.md §8b device list): a bad list is FITOCT_E_ARG with a
+    message, before any device is touched (so also on a host without a GPU)."""
+    from fitoct_amd.api import Plan
+    L = _lib.lib()
+    cfg = SamplerConfig(chains=8, warmup=5, samples=5)
+    c = cfg.to_c()
+    n = len(devices) if n_override is None else n_override
+    c.n_devices = n
+    for i, d in enumerate(devices[:_lib.MAX_DEVICES]):
+        c.devices[i] = d
+    p = _tiny_problem().to_c()
+    h = C.c_void_p()
+    assert L.fitoct_plan_create(C.byref(p), C.byref(c), C.byref(h)) == -1
+    assert msg in L.fitoct_last_error().decode()
+    assert not h.value
+    assert L.fitoct_expgp_sample(C.byref(p), C.byref(c), None) == -1
+    arr = (_lib.Problem * 2)(p, p)
+    assert L.fitoct_batch_create(arr, 2, C.byref(c), C.byref(h)) == -1
+    if n_override is None and len(devices) <= _lib.MAX_DEVICES:
+        with pytest.raises(_lib.FitOCTError) as ei:
+            Plan(_tiny_problem(), SamplerConfig(chains=8, warmup=5, samples=5, devices=devices))
+        assert ei.value.code == -1
+    with pytest.raises(ValueError):
+        SamplerConfig(devices=(0,) * 17).to_c()
+
+
+@pytest.mark.skipif(_lib.lib().fitoct_device_count() > 0, reason="a GPU is visible")
+@pytest.mark.parametrize("entry", ["plan", "sample", "batch"])
+def test_device_list_without_gpu_fails_per_device(entry):
+    """The per-device host threads report their failure to the caller's thread
+    (fitoct_last_error is thread-local): FITOCT_E_NODEVICE naming the device."""
+    from fitoct_amd.api import Batch, Plan, sample
+    cfg = SamplerConfig(chains=5, warmup=5, samples=5, devices=(0, 0, 0))
+    with pytest.raises(_lib.FitOCTError) as ei:
+        if entry == "plan":
+            Plan(_tiny_problem(), cfg)
+        elif entry == "sample":
+            sample(_tiny_problem(), cfg)
+        else:
+            Batch([_tiny_problem()] * 4, cfg)
+    assert ei.value.code == -3 and "device 0" in str(ei.value) and "no HIP device" in str(ei.value)
