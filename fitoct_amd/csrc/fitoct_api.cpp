@@ -430,6 +430,7 @@ void free_plan(fitoct_plan* pl) {
   if (pl->h_cancel) (void)hipHostFree(pl->h_cancel);
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
   if (pl->ev1) (void)hipEventDestroy(pl->ev1);
+  if (pl->own_stream) (void)hipStreamDestroy(pl->own_stream);
   delete pl;
 }
 
@@ -1116,6 +1117,7 @@ void free_batch(fitoct_batch* b) {
   (void)hipFree(b->d_draws);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
+  if (b->own_stream) (void)hipStreamDestroy(b->own_stream);
   delete b;
 }
 }  // namespace

@@ -123,6 +123,15 @@ bool in_place(const void* d_draws, int dev, int gdev) {
   return d_draws && dev == gdev && !force_copy;
 }
 
+// a non-blocking stream on `dev` for one shard: the shards of a group never order
+// against each other, nor against the synchronous status reads / peer copies issued
+// for another shard, through the device's default stream
+int own_stream(int dev, hipStream_t& st) {
+  HIP_TRY(hipSetDevice(dev));
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  return FITOCT_OK;
+}
+
 size_t chain_bytes(const fitoct_plan* sh) {
   return sizeof(double) * (size_t)sh->kp.iters_saved * sh->kp.ncols;
 }
@@ -209,7 +218,9 @@ int group_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
     void* dst = in_place(d_draws, sh->cfg.device, gdev)
                     ? (char*)d_draws + chain_bytes(sh) * (size_t)pl->shard_off[r]
                     : nullptr;
-    const int rc = fitoct_plan_launch(sh, dst, nullptr);
+    int rc = FITOCT_OK;
+    if (!sh->own_stream) rc = own_stream(sh->cfg.device, sh->own_stream);
+    if (!rc) rc = fitoct_plan_launch(sh, dst, sh->own_stream);
     if (rc) {   // stop what was launched before reporting
       const std::string msg = g_last_error;
       for (size_t k = 0; k < r; ++k) {
@@ -393,7 +404,11 @@ int group_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
     fitoct_batch* sb = b->subs[r];
     char* slice = d_draws ? (char*)d_draws + b->per_bytes * (size_t)b->sub_off[r] : nullptr;
     const bool direct = in_place(d_draws, sb->cfg.device, gdev);
-    const int e = fitoct_batch_run(sb, direct ? slice : nullptr, nullptr);
+    if (!sb->own_stream) {
+      const int e = own_stream(sb->cfg.device, sb->own_stream);
+      if (e) return e;
+    }
+    const int e = fitoct_batch_run(sb, direct ? slice : nullptr, sb->own_stream);
     if (e) return e;
     if (d_draws && !direct)
       HIP_TRY(hipMemcpyPeer(slice, gdev, sb->d_draws, sb->cfg.device,

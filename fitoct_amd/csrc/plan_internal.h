@@ -46,6 +46,9 @@ struct fitoct_plan {
   std::vector<int> shard_off;
   void* gather_dst = nullptr;  // caller's d_draws of the launch in flight (or NULL)
   int gather_dev = -1;         // device holding gather_dst
+  // a shard's own non-blocking stream: shards never wait on one another (nor on the
+  // synchronous status reads and peer copies of other shards) through a default stream
+  hipStream_t own_stream = nullptr;
 };
 
 struct fitoct_batch {
@@ -65,6 +68,7 @@ struct fitoct_batch {
   std::vector<fitoct_batch*> subs;
   std::vector<int> sub_off;
   int n_problems = 0;
+  hipStream_t own_stream = nullptr;   // a sub-batch's own non-blocking stream
 };
 
 namespace fitoct {
