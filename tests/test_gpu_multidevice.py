@@ -201,6 +201,8 @@ def test_rshim_driver_csv_over_devices(tmp_path):
     from test_rshim_driver import _drive_csv
     prob = _prob("horseshoe", 512, 10)
     cfg = SamplerConfig(chains=5, warmup=100, samples=100, seed=21, max_treedepth=8)
+    (tmp_path / "one").mkdir()
+    (tmp_path / "two").mkdir()
     rc1, p1, lines1 = _drive_csv(prob, cfg, tmp_path / "one")
     rc2, p2, lines2 = _drive_csv(prob, dataclasses.replace(cfg, devices=(0, 0)), tmp_path / "two")
     assert rc1 == 0 and rc2 == 0, _lib.lib().fitoct_last_error()
