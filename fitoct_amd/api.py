@@ -436,7 +436,7 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
              nb_iter=1000, prior_PD=0, open_progress=False, *, nb_chains=4,
              prior_type="normal", lambda_scale=10.0, nu=1.0, adapt_delta=0.8,
              max_treedepth=10, seed=None, precision="f64", device=0, n_gpus=None,
-             refresh=1, **model_switches):
+             devices=None, refresh=1, **model_switches):
     """Drop-in for ``FitOCTLib::fitExpGP`` (FitOCT.R:110-124).
 
     ``nb_iter`` counts warmup + sampling iterations, as the callers pass
@@ -450,7 +450,8 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
     stdout sink, server.R:391-393,457-484); ``refresh=0`` silences them.
     ``n_gpus`` (replaces ``options(mc.cores = detectCores())``,
     FitOCT.R:13): the chains are split over devices ``device .. device + n_gpus - 1``
-    (the library runs one host thread per device; the draws do not depend on it).
+    (the library runs one host thread per device; the draws do not depend on it);
+    ``devices`` gives the ordinals explicitly instead (repeats allowed).
     Returns ``dict(fit, method, xGP, prior_PD, lasso)``.
     """
     from .stanfit import StanFit
@@ -480,7 +481,8 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
                 fit.par[k] = g[k][0]
         return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,
                 "lasso": prior_type == "lasso"}
-    devices = tuple(range(int(device), int(device) + int(n_gpus))) if n_gpus and n_gpus > 1 else ()
+    if devices is None:
+        devices = tuple(range(int(device), int(device) + int(n_gpus))) if n_gpus and n_gpus > 1 else ()
     cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_sample, seed=seed,
                         adapt_delta=adapt_delta, max_treedepth=max_treedepth,
                         precision=precision, device=device, devices=devices)

@@ -216,11 +216,19 @@ def test_rshim_driver_csv_over_devices(tmp_path):
 
 
 def test_fitexpgp_n_gpus():
-    """fitExpGP(..., n_gpus=2): the Python mirror of the R argument."""
+    """fitExpGP(..., n_gpus=k) (the Python mirror of the R argument) takes devices
+    0..k-1: every GPU of this box gives the one-device draws, an explicit repeated list
+    too, and asking for more GPUs than exist is FITOCT_E_ARG naming the device."""
     from fitoct_amd.api import fitExpGP
     p = _prob("normal", 400, 8)
     kw = dict(dataType=2, Nn=8, gridType="extremal", theta0=p.theta0, Sigma0=p.Sigma0,
               nb_warmup=60, nb_iter=120, nb_chains=6, seed=77, refresh=0)
+    n = _lib.lib().fitoct_device_count()
     a = fitExpGP(p.x, p.y, p.uy, **kw)
-    b = fitExpGP(p.x, p.y, p.uy, n_gpus=3, **kw)
+    b = fitExpGP(p.x, p.y, p.uy, n_gpus=n, **kw)
+    c = fitExpGP(p.x, p.y, p.uy, devices=(0, 0, 0), **kw)
     np.testing.assert_array_equal(a["fit"]._draws, b["fit"]._draws)
+    np.testing.assert_array_equal(a["fit"]._draws, c["fit"]._draws)
+    with pytest.raises(_lib.FitOCTError) as ei:
+        fitExpGP(p.x, p.y, p.uy, n_gpus=n + 1, **kw)
+    assert ei.value.code == -1 and f"device {n}" in str(ei.value)
