@@ -69,6 +69,17 @@ enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2, FAM_MONO = 3 };
 #ifndef FITOCT_PAIRED_BINS
 #define FITOCT_PAIRED_BINS 1
 #endif
+// 16 bins per lane (config 4): bins in groups of FITOCT_BPT16_GROUP whose moments are
+// formed per group, and (FITOCT_BPT16_PAIRS) pairs sharing one reciprocal
+#ifndef FITOCT_BPT16_GROUP
+#define FITOCT_BPT16_GROUP 8
+#endif
+#ifndef FITOCT_BPT16_PAIRS
+#define FITOCT_BPT16_PAIRS 0
+#endif
+#ifndef FITOCT_BPT16_OPAQUE
+#define FITOCT_BPT16_OPAQUE 1
+#endif
 
 // Cycle stamps (FITOCT_STAMPS) exist only in a profiling build
 // (FITOCT_PROFILE=1 python -m fitoct_amd.build): the production kernels carry
@@ -722,19 +733,37 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
     for (int k = 0; k < 4 + NNP; ++k) acc[k] = 0.0;
     R umin = R(1);
     if constexpr (BPT == 16) {   // MODE_POLY f64 on an arithmetic grid (host-checked)
-      const double cx0 = bins.cx[0], t0 = bins.row[0][0], tmax = P.geo_tmax;
+      double cx0 = bins.cx[0], t0 = bins.row[0][0];
+      const double tmax = P.geo_tmax;
+      // opaque per sweep: c*x_b and t_b are formed inside the sweep, as the compact layout
+      // intends, instead of being hoisted out of the sweep loop (32 more live doubles)
+      if constexpr (FITOCT_BPT16_OPAQUE) asm volatile("" : "+v"(cx0), "+v"(t0));
+      // the lane's bins in groups of NQ (moments per group: NQ weights live at a time)
+      constexpr int NQ = FITOCT_BPT16_GROUP;
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        double w[8];
+      for (int q = 0; q < 16 / NQ; ++q) {
+        double w[NQ];
+        if constexpr (FITOCT_BPT16_PAIRS) {
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          const int bb = half * 8 + b;
-          const double cxb = cx0 + P.geo_dcx[bb];
-          const double tb = fmin(t0 * P.geo_R[bb], tmax);
-          w[b] = bin_poly_fwd<R, NNP, double>(cxb, bins.y[bb], bins.isu[bb], tb,
-                                              bins.row[bb][1], th1, th2, th3, cf, acc, umin);
+          for (int b = 0; b < NQ; b += 2) {
+            const int bb = q * NQ + b;
+            bin_poly_fwd2<R, NNP, double>(cx0 + P.geo_dcx[bb], bins.y[bb], bins.isu[bb],
+                                          fmin(t0 * P.geo_R[bb], tmax), bins.row[bb][1],
+                                          cx0 + P.geo_dcx[bb + 1], bins.y[bb + 1], bins.isu[bb + 1],
+                                          fmin(t0 * P.geo_R[bb + 1], tmax), bins.row[bb + 1][1],
+                                          th1, th2, th3, cf, acc, umin, w[b], w[b + 1]);
+          }
+        } else {
+#pragma unroll
+          for (int b = 0; b < NQ; ++b) {
+            const int bb = q * NQ + b;
+            const double cxb = cx0 + P.geo_dcx[bb];
+            const double tb = fmin(t0 * P.geo_R[bb], tmax);
+            w[b] = bin_poly_fwd<R, NNP, double>(cxb, bins.y[bb], bins.isu[bb], tb,
+                                                bins.row[bb][1], th1, th2, th3, cf, acc, umin);
+          }
         }
-        moments_geo_add<8, NNP>(P, half ? t0 * P.geo_R[8] : t0, w, acc);
+        moments_geo_add<NQ, NNP>(P, q ? t0 * P.geo_R[q * NQ] : t0, w, acc);
       }
     } else if constexpr (BPT > 0 && MODE == MODE_POLY && sizeof(R) == 8) {
       if (P.geo) {
