@@ -412,6 +412,9 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
 int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chains,
                 int force_bpt, fitoct_plan** out);
 
+// tiles of several chains speculate once they host <= this many live chains
+constexpr int kSpecLiveDefault = 2;
+
 void free_plan(fitoct_plan* pl) {
   if (!pl) return;
   for (fitoct_plan* sh : pl->shards) free_plan(sh);
@@ -744,15 +747,22 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
     k.mig_tiles = T;
     k.mig_img_words = words;
   }
-  // speculative leaves (nuts_device.hip leaf_spec) in tiles of one chain, where a spare
-  // NUTS wave helps it (config 2 +4 %).  Tiles of several chains have no spare wave and
-  // lose 10 % with it (config 5), so they run the plain sampler unless FITOCT_SPEC=1
-  // (tests; any plan without migration).  FITOCT_NO_SPEC=1: the plain sampler always.
+  // Speculative leaves (nuts_device.hip leaf_spec).  A tile of one chain always
+  // speculates, with a spare NUTS wave helping (config 2 +4 %).  A tile of several chains
+  // has no spare wave: while it hosts more than k.spec_live live chains the sweep hides
+  // the sampler's latency and speculation only adds work (config 5 -10 % with it always
+  // on), so a chain speculates only once its tile has thinned out to <= spec_live chains
+  // (the launch's tail, where migration leaves tiles of 1-2 chains).  Draws are the same
+  // bit for bit either way.  FITOCT_SPEC_LIVE=n overrides spec_live (0: never; GMAX:
+  // always), FITOCT_SPEC=1 is FITOCT_SPEC_LIVE=GMAX (tests), FITOCT_NO_SPEC=1 builds the
+  // plain sampler.
   {
-    const char* fs = getenv("FITOCT_SPEC");
-    bool on = pl->mig_bytes == 0 && (fs != nullptr ? atoi(fs) != 0 : k.G == 1);
-    if (getenv("FITOCT_NO_SPEC") != nullptr) on = false;
-    k.spec = on ? 1 : 0;
+    int live = k.G == 1 ? 1 : kSpecLiveDefault;
+    if (const char* fs = getenv("FITOCT_SPEC")) live = atoi(fs) != 0 ? GMAX : live;
+    if (const char* fl = getenv("FITOCT_SPEC_LIVE")) live = atoi(fl);
+    if (getenv("FITOCT_NO_SPEC") != nullptr) live = 0;
+    k.spec_live = std::max(0, std::min(live, GMAX));
+    k.spec = k.spec_live > 0 ? 1 : 0;
   }
   *out = guard.release();
   return FITOCT_OK;
@@ -771,7 +781,8 @@ int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
     info->chains = pl->kp.chains;
     info->tiles = pl->tiles;
     info->chains_per_tile = pl->kp.G;
-    info->sampler = pl->mig_bytes > 0 ? FITOCT_SAMPLER_MIGRATE
+    info->sampler = pl->mig_bytes > 0
+                        ? (pl->kp.spec ? FITOCT_SAMPLER_MIGRATE_SPEC : FITOCT_SAMPLER_MIGRATE)
                     : pl->kp.spec ? FITOCT_SAMPLER_SPECULATIVE : FITOCT_SAMPLER_PLAIN;
     info->n_devices = 1;
     info->bins_per_thread = pl->bpt;

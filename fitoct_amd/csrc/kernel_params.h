@@ -99,7 +99,9 @@ struct KParams {
   double* mig_img;          // [tiles * GMAX][mig_img_words] chain images in flight
   int mig_tiles, mig_img_words;
   int nuts_prio;            // s_setprio of the NUTS waves (0..3)
-  int spec;                 // 1: speculative leaves with a helper wave (one chain per tile)
+  int spec;                 // 1: the speculative-leaf sampler (nuts_device.hip leaf_spec)
+  int spec_live;            // ... a chain speculates while its tile hosts <= spec_live live
+                            // chains (tiles of one chain: always, with a helper wave)
   // ---- run-time progress / cancellation (host-pinned; nullptr: off) ----
   int* progress;            // [chains] transitions completed (written at each boundary)
   const int* cancel;        // != 0: every chain stops at its next checked boundary

@@ -107,6 +107,7 @@ enum VecId : int {
   V_RHO, V_PNEAR,              // trajectory momentum sum, near end of old trajectory
   V_QS, V_QE,                  // staged q and its constrained values (exp on positive params)
   V_PG, V_CA,                  // prior part of grad, likelihood coefficient (prior_part)
+  V_KQ, V_KP, V_KG,            // a speculated leaf's q, end-updated p, g (migrating sampler)
   NVEC
 };
 // U-turn record of one tree level (LDS)
@@ -865,11 +866,18 @@ struct Chain {
   double krow[KROW ? NNP : 1];
   const AS_LDS double* bv;
   int lane, slot, lc, gid, nct;
-  static constexpr bool spec = SPEC && !MIG;   // speculative leaves (the SPEC sampler)
-  bool helped;   // ... with a helper wave (tiles of one chain); else this wave does its part
+  // speculative leaves (the SPEC sampler): always in a tile of one chain (with a helper
+  // wave), else while the tile hosts <= P.spec_live live chains (the tail of a launch, when
+  // the sweep no longer hides the sampler's latency; this wave then does the helper's part)
+  static constexpr bool spec = SPEC;
+  bool helped;   // ... with a helper wave (tiles of one chain, no migration)
+  const AS_LDS int* live = nullptr;   // the tile's live-chain count (kernel-maintained)
   // a speculated leaf's values, kept from leaf_spec to act_spec_book (across the hand-off)
-  V k_q, k_pe, k_g, k_minv, k_ps, k_gs;
-  double k_lp, k_s2, k_en;
+  // (the metric and the next subtree's start are re-read from LDS; in the migrating
+  // sampler, whose migration paths leave no registers to spare, the leaf itself too)
+  static constexpr bool KLDS = MIG;
+  V k_q, k_pe, k_g;
+  // (its lp / sum r^2 stay in Sp->cur_lp / cur_s2 until the bookkeeping)
   int k_dirn, k_dn, k_jn;
   uint32_t k_t;
   // the helper publishes the booked leaf's weight by writing request numbers here
@@ -883,7 +891,7 @@ struct Chain {
         part(L.part()), Kinv(L.kinv()), bv(L.bv()),
         lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
     gid = Pr().chain_offset + lc;
-    helped = spec && nct_ == 1;
+    helped = SPEC && !MIG && nct_ == 1;
     key = make_key(Pr().seed, (uint32_t)gid);
     if constexpr (KROW) {
       const int r = lane < NNP ? lane : 0;
@@ -1297,7 +1305,10 @@ struct Chain {
       st(V_CUR_G, g);
       Sp->cur_lp = lp;
       Sp->cur_s2 = s0;
-      if constexpr (spec) return leaf_spec(q, p, g, minv, lp, s0);
+      if constexpr (spec) {   // per leaf: plain and speculative leaves leave the same state
+        if (helped || uni(__atomic_load_n(live, __ATOMIC_RELAXED)) <= Pr().spec_live)
+          return leaf_spec(q, p, g, minv, lp, s0);
+      }
       return leaf(q, p, g, minv, lp, s0);
     }
     const double lp = finish_grad(g, s0);
@@ -1621,8 +1632,14 @@ struct Chain {
     // for the helper (spec_weight): the booked leaf's end-updated momentum, in CUR_G's
     // slot (while a tree grows nothing reads CUR_G; begin_subtree rewrites it)
     st(V_CUR_G, pe);   // (its lp is Sp->cur_lp, set by act_grad)
-    k_q = q; k_pe = pe; k_g = g; k_minv = minv; k_ps = ps; k_gs = gs;
-    k_lp = cur_lp; k_s2 = cur_s2; k_en = en;
+    if constexpr (KLDS) {
+      st(V_KQ, q);
+      st(V_KP, pe);
+      st(V_KG, g);
+    } else {
+      k_q = q; k_pe = pe; k_g = g;
+    }
+
     k_dirn = dirn; k_dn = dn; k_jn = jn; k_t = t;
     return A_SPEC_STAGED;   // the kernel enqueues the position and posts the helper
   }
@@ -1630,16 +1647,22 @@ struct Chain {
   __device__ int act_spec_book() {
     FITOCT_MARK(act_spec_book);
     if (!helped) spec_weight();   // no helper wave in a tile of several chains
-    const int r = leaf_book_split(k_q, k_pe, k_g, k_minv, k_lp, k_s2);
+    const int r = KLDS ? leaf_book_split(ld(V_KQ), ld(V_KP), ld(V_KG), ld(V_MINV), Sp->cur_lp,
+                                         Sp->cur_s2)
+                       : leaf_book_split(k_q, k_pe, k_g, ld(V_MINV), Sp->cur_lp, Sp->cur_s2);
     if (r == LB_NEXT) {   // the rest of act_begin_subtree (the top merge set depth d + 1)
+      // the next subtree grows from trajectory end k_dirn: the far end if the direction
+      // changed (untouched by the top merge), else the end the top merge just set to this
+      // leaf -- in both cases the (p, g) leaf_spec staged the next leapfrog from
       Sp->dir = k_dirn;
-      st(V_PNEAR, k_ps);
-      st(V_CUR_G, k_gs);
+      const int eq = k_dirn ? V_E1_Q : V_E0_Q;
+      st(V_PNEAR, ld(eq + 1));
+      st(V_CUR_G, ld(eq + 2));
       Sp->cur_lp = Sp->end_lp[k_dirn];
       Sp->cur_s2 = Sp->end_s2[k_dirn];
       Sp->leaf = 0;
       if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;
-      Sp->lf_e = k_en;
+      Sp->lf_e = k_dirn ? Sp->eps_used : -Sp->eps_used;
     }
     // without a helper, the next position's prior part follows the bookkeeping here
     if (!helped && r != LB_END) prior_and_uniforms(true, k_dn, k_jn, k_t);
@@ -2278,13 +2301,15 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   // request {depth, leaf, iteration} for the prior part of a speculated position; the
   // helper wave (slot 1) runs it and publishes the request number it finished
   __shared__ int help_req, help_done, help_wdone, help_arg[3];
-  const bool spec = SPEC && !MIG;
-  const bool helped = spec && nct == 1;   // a spare NUTS wave helps the tile's one chain
+  const bool spec = SPEC;
+  const bool helped = SPEC && !MIG && nct == 1;   // a spare NUTS wave helps the tile's one chain
+  __shared__ int live_chains;   // chains the tile hosts (speculation policy, Chain::live)
 
   load_kinv<PPL, NNP>(P, L, tid);
   if (tid == 0) {
     q_reserve = 0;
     n_active = nct;
+    live_chains = nct;
     help_req = 0;
     help_done = 0;
     help_wdone = 0;
@@ -2430,6 +2455,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       for (;;) {   // the slot's own chain, then (migration) chains handed over by other tiles
        if (lc >= 0) {
         Ch ch(P, L, c, lc, lane, nct);
+        ch.live = (const AS_LDS int*)&live_chains;
         long long steps = 0;
         bool in_sweep = false;   // the last run() was A_PRIOR, overlapping the chain's sweep
         // ONE call site of the action machine (it is inlined once, not per caller)
@@ -2545,6 +2571,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             atomicAdd(&chains_done_here, 1);
           }
           if (helped && lane == 0) __atomic_store_n(&help_req, -1, __ATOMIC_RELAXED);   // release the helper
+          if (spec && lane == 0) atomicSub(&live_chains, 1);
           break;
         }
         if (++steps > P.max_steps) {   // termination guarantee: report, never hang
@@ -2589,6 +2616,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if (!mig) break;
         lc = receive_chain<PPL>(P, L, c, lane);
         if (lc < 0) break;
+        if (spec && lane == 0) atomicAdd(&live_chains, 1);
         a = Ch::A_START_TRANSITION;
       }
       wave_fence();
@@ -2708,7 +2736,10 @@ static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int t
     hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP);
   } else {
     // three samplers: with migration, with speculative leaves (one chain per tile), plain
-    auto k = P.mig != nullptr ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, true, false>
+    // four samplers: with / without migration, with / without speculative leaves
+    auto k = P.mig != nullptr
+                 ? (P.spec ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, true, true>
+                           : nuts_kernel<R, BPT, NNP, PPL, MODE, F, true, false>)
              : P.spec ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, false, true>
                       : nuts_kernel<R, BPT, NNP, PPL, MODE, F, false, false>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

@@ -154,16 +154,18 @@ typedef struct fitoct_plan_info {
   int32_t n_devices;       /* devices the plan's chains (a batch's problems) run on */
 } fitoct_plan_info;
 
-/* fitoct_plan_info::sampler.  PLAIN: tiles of several chains, or migration off;
+/* fitoct_plan_info::sampler.  PLAIN: no speculation, no migration;
  * MIGRATE: chains move between tiles at transition boundaries (work balance);
- * SPECULATIVE: one chain per tile (or FITOCT_SPEC=1 on any plan without migration);
- * each chain's next leapfrog position is swept while the current leaf's tree
- * bookkeeping runs, with a spare wave's help in a tile of one chain (FITOCT_NO_SPEC=1
- * turns it off).  The draws
- * are the same bit for bit whichever variant runs. */
+ * SPECULATIVE: speculative leaves -- a chain's next leapfrog position is swept while the
+ * current leaf's tree bookkeeping runs: always in a tile of one chain (a spare wave
+ * helps), and in tiles of several chains once they have thinned out to <= 2 live chains
+ * (the launch's tail);
+ * MIGRATE_SPEC: both (the headline shape).  FITOCT_NO_SPEC=1 / FITOCT_NO_MIGRATE=1 turn
+ * either off.  The draws are the same bit for bit whichever variant runs. */
 #define FITOCT_SAMPLER_PLAIN 0
 #define FITOCT_SAMPLER_MIGRATE 1
 #define FITOCT_SAMPLER_SPECULATIVE 2
+#define FITOCT_SAMPLER_MIGRATE_SPEC 3
 
 typedef struct fitoct_plan fitoct_plan;
 

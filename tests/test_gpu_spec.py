@@ -3,7 +3,8 @@ with one chain per tile the next leapfrog position is swept while the current le
 merges and U-turn checks run, and a helper wave computes its prior part.  The draws
 must equal the plain sampler's (FITOCT_NO_SPEC=1) bit for bit, trajectory ends
 (discarded speculations) included, for every prior family; likewise in tiles of
-several chains that do not migrate, where there is no helper wave."""
+several chains, migrating or not, where there is no helper wave and a chain speculates
+only while its tile has thinned out (or at every leaf with FITOCT_SPEC=1)."""
 from __future__ import annotations
 
 import os
@@ -46,11 +47,42 @@ def test_speculative_leaves_preserve_draws_bitwise(family, N, depth):
     assert a.total_leapfrogs == b.total_leapfrogs
 
 
-def test_migrating_plans_do_not_speculate():
-    prob = _prob("normal", 512, 15)
-    cfg = SamplerConfig(chains=1024, warmup=10, samples=10, seed=3, max_treedepth=6)
-    with Plan(prob, cfg) as pl:
-        assert pl.info["chains_per_tile"] == 4 and pl.info["sampler"] == 1   # MIGRATE
+def _run_env(prob, cfg, **env):
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        for k, v in env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        with Plan(prob, cfg) as pl:
+            pl.run()
+            return pl.info, pl.download()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("live", ["2", "4"])
+def test_migrating_plans_speculate_in_the_tail_bitwise(live):
+    """The headline sampler (MIGRATE_SPEC): tiles of four migrating chains speculate once
+    they host <= 2 live chains (the launch's tail; FITOCT_SPEC_LIVE=4: at every leaf), a
+    chain switching paths leaf by leaf and moving between tiles.  Same draws, step sizes,
+    metrics and leapfrog counts as the plain migrating sampler."""
+    prob = _prob("horseshoe", 2048, 15)
+    cfg = SamplerConfig(chains=1024, warmup=60, samples=40, seed=3, max_treedepth=7)
+    info, a = _run_env(prob, cfg, FITOCT_SPEC_LIVE=live, FITOCT_NO_SPEC=None)
+    info0, b = _run_env(prob, cfg, FITOCT_SPEC_LIVE=None, FITOCT_NO_SPEC="1")
+    assert info["chains_per_tile"] == 4 and info["sampler"] == 3   # MIGRATE_SPEC
+    assert info0["sampler"] == 1                                   # MIGRATE
+    np.testing.assert_array_equal(a.draws, b.draws)
+    np.testing.assert_array_equal(a.stepsize, b.stepsize)
+    np.testing.assert_array_equal(a.inv_metric, b.inv_metric)
+    assert a.total_leapfrogs == b.total_leapfrogs
+    assert a.migrations > 0 and b.migrations > 0
 
 
 def test_tiles_of_several_chains_speculate_without_helper_bitwise():

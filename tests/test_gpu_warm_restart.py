@@ -104,7 +104,7 @@ def test_warm_restart_chain_addressing_across_kernels():
     cfg = SamplerConfig(chains=600, warmup=0, samples=15, seed=32, max_treedepth=6,
                         adapt_engaged=False)
     with Plan(prob, cfg) as pl:
-        assert pl.info["chains_per_tile"] >= 2 and pl.info["sampler"] == 1   # MIGRATE
+        assert pl.info["chains_per_tile"] >= 2 and pl.info["sampler"] == 3   # MIGRATE_SPEC
         pl.set_init(prev.last_q, prev.stepsize, prev.inv_metric)
         pl.run()
         big = pl.download()
