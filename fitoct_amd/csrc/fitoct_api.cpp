@@ -412,8 +412,13 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
 int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chains,
                 int force_bpt, fitoct_plan** out);
 
-// tiles of several chains speculate once they host <= this many live chains
-constexpr int kSpecLiveDefault = 2;
+// Migrating tiles of several chains speculate once they host <= this many live chains.
+// Measured on config 3 at full length (profiles/r03_ab_spec_live.txt, two interleaved
+// runs each): 0 (no speculation) 119.1 k draws/s, 1: 119.7-120.2 k, 2: 121.2-121.4 k,
+// 3: 121.5-122.0 k, 4 (always): 119.5-120.3 k.  Tiles that do not migrate (batch mode,
+// config 5) lose 7 % with any tail speculation (the speculative kernel's extra registers
+// and per-leaf policy read), so they do not speculate.
+constexpr int kSpecLiveMigrating = 3;
 
 void free_plan(fitoct_plan* pl) {
   if (!pl) return;
@@ -749,15 +754,14 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   }
   // Speculative leaves (nuts_device.hip leaf_spec).  A tile of one chain always
   // speculates, with a spare NUTS wave helping (config 2 +4 %).  A tile of several chains
-  // has no spare wave: while it hosts more than k.spec_live live chains the sweep hides
-  // the sampler's latency and speculation only adds work (config 5 -10 % with it always
-  // on), so a chain speculates only once its tile has thinned out to <= spec_live chains
-  // (the launch's tail, where migration leaves tiles of 1-2 chains).  Draws are the same
-  // bit for bit either way.  FITOCT_SPEC_LIVE=n overrides spec_live (0: never; GMAX:
+  // has no spare wave: while it hosts 4 live chains the sweep hides the sampler's latency
+  // and speculation only adds work, so a migrating chain speculates only once its tile has
+  // thinned out to <= kSpecLiveMigrating chains (the launch's tail, config 3 +2 %).  Draws
+  // are the same bit for bit either way.  FITOCT_SPEC_LIVE=n overrides spec_live (0: never; GMAX:
   // always), FITOCT_SPEC=1 is FITOCT_SPEC_LIVE=GMAX (tests), FITOCT_NO_SPEC=1 builds the
   // plain sampler.
   {
-    int live = k.G == 1 ? 1 : kSpecLiveDefault;
+    int live = k.G == 1 ? 1 : pl->mig_bytes > 0 ? kSpecLiveMigrating : 0;
     if (const char* fs = getenv("FITOCT_SPEC")) live = atoi(fs) != 0 ? GMAX : live;
     if (const char* fl = getenv("FITOCT_SPEC_LIVE")) live = atoi(fl);
     if (getenv("FITOCT_NO_SPEC") != nullptr) live = 0;

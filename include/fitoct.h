@@ -158,8 +158,8 @@ typedef struct fitoct_plan_info {
  * MIGRATE: chains move between tiles at transition boundaries (work balance);
  * SPECULATIVE: speculative leaves -- a chain's next leapfrog position is swept while the
  * current leaf's tree bookkeeping runs: always in a tile of one chain (a spare wave
- * helps), and in tiles of several chains once they have thinned out to <= 2 live chains
- * (the launch's tail);
+ * helps), and in migrating tiles of several chains once they have thinned out to <= 3
+ * live chains (the launch's tail);
  * MIGRATE_SPEC: both (the headline shape).  FITOCT_NO_SPEC=1 / FITOCT_NO_MIGRATE=1 turn
  * either off.  The draws are the same bit for bit whichever variant runs. */
 #define FITOCT_SAMPLER_PLAIN 0
