@@ -107,7 +107,6 @@ enum VecId : int {
   V_RHO, V_PNEAR,              // trajectory momentum sum, near end of old trajectory
   V_QS, V_QE,                  // staged q and its constrained values (exp on positive params)
   V_PG, V_CA,                  // prior part of grad, likelihood coefficient (prior_part)
-  V_KQ, V_KP, V_KG,            // a speculated leaf's q, end-updated p, g (migrating sampler)
   NVEC
 };
 // U-turn record of one tree level (LDS)
@@ -873,8 +872,12 @@ struct Chain {
   bool helped;   // ... with a helper wave (tiles of one chain, no migration)
   const AS_LDS int* live = nullptr;   // the tile's live-chain count (kernel-maintained)
   // a speculated leaf's values, kept from leaf_spec to act_spec_book (across the hand-off)
-  // (the metric and the next subtree's start are re-read from LDS; in the migrating
-  // sampler, whose migration paths leave no registers to spare, the leaf itself too)
+  // (the metric and the next subtree's start are re-read from LDS.)  The migrating
+  // sampler, whose migration paths leave no registers to spare, also parks the leaf itself
+  // in LDS, in slots dead from leaf_spec to the end of the bookkeeping: q in V_PG and g in
+  // V_CA (there is no helper wave, so the next prior part is written only after the
+  // bookkeeping), the end-updated p in V_CUR_G (where spec_weight reads it anyway).  No
+  // LDS is added: the tile's LDS carve decides how many chains fit (G = 4 at depth 12).
   static constexpr bool KLDS = MIG;
   V k_q, k_pe, k_g;
   // (its lp / sum r^2 stay in Sp->cur_lp / cur_s2 until the bookkeeping)
@@ -1633,9 +1636,8 @@ struct Chain {
     // slot (while a tree grows nothing reads CUR_G; begin_subtree rewrites it)
     st(V_CUR_G, pe);   // (its lp is Sp->cur_lp, set by act_grad)
     if constexpr (KLDS) {
-      st(V_KQ, q);
-      st(V_KP, pe);
-      st(V_KG, g);
+      st(V_PG, q);
+      st(V_CA, g);
     } else {
       k_q = q; k_pe = pe; k_g = g;
     }
@@ -1647,7 +1649,7 @@ struct Chain {
   __device__ int act_spec_book() {
     FITOCT_MARK(act_spec_book);
     if (!helped) spec_weight();   // no helper wave in a tile of several chains
-    const int r = KLDS ? leaf_book_split(ld(V_KQ), ld(V_KP), ld(V_KG), ld(V_MINV), Sp->cur_lp,
+    const int r = KLDS ? leaf_book_split(ld(V_PG), ld(V_CUR_G), ld(V_CA), ld(V_MINV), Sp->cur_lp,
                                          Sp->cur_s2)
                        : leaf_book_split(k_q, k_pe, k_g, ld(V_MINV), Sp->cur_lp, Sp->cur_s2);
     if (r == LB_NEXT) {   // the rest of act_begin_subtree (the top merge set depth d + 1)

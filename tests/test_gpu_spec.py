@@ -129,3 +129,15 @@ def test_batch_speculates_bitwise():
                 os.environ[k] = v
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x.draws, y.draws)
+
+
+def test_headline_tiles_fit_four_chains_at_depth_12():
+    """The LDS carve of a tile decides how many chains it hosts: the headline shape must
+    keep four chains per tile (1024 chains on 256 CUs, migration on) under the
+    hard-geometry profile's max_treedepth 12 too (bench.py hard_geometry)."""
+    prob = _prob("horseshoe", 2048, 15)
+    for depth in (10, 12):
+        cfg = SamplerConfig(chains=1024, warmup=10, samples=10, seed=3, max_treedepth=depth)
+        with Plan(prob, cfg) as pl:
+            assert pl.info["chains_per_tile"] == 4, (depth, pl.info)
+            assert pl.info["sampler"] == 3 and pl.info["lds_bytes"] <= 160 * 1024
