@@ -49,7 +49,9 @@ CONFIGS = {
 }
 FP64_VALU_PEAK_TF = 78.6          # MI355X FP64 vector peak (vendor spec; 1/2 of FP32 vector)
 HBM_PEAK_GBS = 8000.0
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+# PMC traffic summaries (scripts/pmc_traffic.sh [config]), newest round first, matched to
+# a bench line by its workload string
+TRAFFIC_GLOB = os.path.join(ROOT, "profiles", "r*_pmc_traffic*.json")
 
 
 def f_grad(N, Nn):
@@ -173,13 +175,16 @@ def convergence(draws, W_saved, cols):
 
 
 def load_traffic(workload):
-    try:
-        with open(TRAFFIC_FILE) as f:
-            t = json.load(f)
+    import glob
+    for path in sorted(glob.glob(TRAFFIC_GLOB), reverse=True):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
         if t.get("workload") == workload:
+            t["source"] = os.path.relpath(path, ROOT)
             return t
-    except (OSError, ValueError):
-        pass
     return None
 
 
@@ -329,7 +334,7 @@ def main():
     if traffic:
         roof["hbm_gbs"] = round(traffic["bytes_per_launch"] / (kms / 1e3) / 1e9, 2)
         roof["hbm_frac"] = round(roof["hbm_gbs"] / HBM_PEAK_GBS, 5)
-        roof["traffic_source"] = os.path.relpath(TRAFFIC_FILE, ROOT)
+        roof["traffic_source"] = traffic["source"]
 
     line = {
         "metric": ("posterior draws/sec (all chains), ExpGP N=2048 @ 1024 chains; R-hat"
@@ -531,6 +536,13 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
                      "traffic": None, "kernel": "nuts_kernel (batched)",
                      "kernel_ms": round(kernel_ms, 2), "gradients_per_launch_rank0": lf},
     }
+    traffic = load_traffic(line["config"]["workload"])
+    if traffic:
+        r = line["roofline"]
+        r["traffic"] = traffic["bytes_per_launch"]
+        r["hbm_gbs"] = round(traffic["bytes_per_launch"] / (kernel_ms / 1e3) / 1e9, 2)
+        r["hbm_frac"] = round(r["hbm_gbs"] / HBM_PEAK_GBS, 5)
+        r["traffic_source"] = traffic["source"]
     for b in batches:
         b.close()
     if rank == 0:

@@ -1566,10 +1566,12 @@ struct Chain {
     AS_GLB double* dp = pslot(sl, P_P);
     AS_GLB double* dg = pslot(sl, P_G);
 #pragma unroll
-    for (int s = 0; s < PPL; ++s) {   // HBM stores, never waited on
-      dq[idx(s)] = q.a[s];
-      dp[idx(s)] = p.a[s];
-      dg[idx(s)] = g.a[s];
+    for (int s = 0; s < PPL; ++s) {   // HBM stores, never waited on; D lanes only (the
+      if (ok(s)) {                    // padding lanes of q, p, g are 0: top_merge reads 0)
+        dq[idx(s)] = q.a[s];
+        dp[idx(s)] = p.a[s];
+        dg[idx(s)] = g.a[s];
+      }
     }
     Sp->pool_lp[sl] = lp;
     Sp->pool_s2[sl] = s2;
@@ -1715,9 +1717,9 @@ struct Chain {
         V q2, p2, g2;
 #pragma unroll
         for (int s = 0; s < PPL; ++s) {
-          q2.a[s] = sq[idx(s)];
-          p2.a[s] = sp[idx(s)];
-          g2.a[s] = sg[idx(s)];
+          q2.a[s] = ok(s) ? sq[idx(s)] : 0.0;
+          p2.a[s] = ok(s) ? sp[idx(s)] : 0.0;
+          g2.a[s] = ok(s) ? sg[idx(s)] : 0.0;
         }
         st(V_SMP_Q, q2);
         st(V_SMP_P, p2);
