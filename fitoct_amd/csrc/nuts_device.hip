@@ -77,6 +77,9 @@ enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2, FAM_MONO = 3 };
 #ifndef FITOCT_BPT16_PAIRS
 #define FITOCT_BPT16_PAIRS 0
 #endif
+#ifndef FITOCT_NT_DRAWS
+#define FITOCT_NT_DRAWS 1
+#endif
 #ifndef FITOCT_BPT16_OPAQUE
 #define FITOCT_BPT16_OPAQUE 1
 #endif
@@ -151,12 +154,6 @@ __device__ __forceinline__ void wave_fence() {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int g_load(AS_GLB int* p) {
   return __hip_atomic_load((int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int g_load_acq(AS_GLB int* p) {
-  return __hip_atomic_load((int*)p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void g_store_rel(AS_GLB int* p, int v) {
-  __hip_atomic_store((int*)p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ int g_add(AS_GLB int* p, int v) {
   return __hip_atomic_fetch_add((int*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1945,6 +1942,14 @@ struct Chain {
     return LB_NEXT;
   }
 
+  // Draw records are written once and never read by the kernel: streaming (non-temporal)
+  // stores, so the draws stream through L2 instead of evicting the proposal pools, whose
+  // lines are rewritten at every other leaf (config 3: L2->memory writes 6.6x the draws
+  // with ordinary stores, profiles/r03_pmc_traffic_config3.json).
+  static __device__ __forceinline__ void st_draw(AS_GLB double* p, double v) {
+    if constexpr (FITOCT_NT_DRAWS) __builtin_nontemporal_store(v, p);
+    else *p = v;
+  }
   __device__ void write_draw(double accept, double energy) const {
     const int t = Sp->t, W = Pr().warmup;
     if (t < W && !Pr().save_warmup) return;
@@ -1954,7 +1959,7 @@ struct Chain {
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
-      if (k < Pr().D) rec[7 + k] = is_log(k) ? exp(q.a[s]) : q.a[s];
+      if (k < Pr().D) st_draw(&rec[7 + k], is_log(k) ? exp(q.a[s]) : q.a[s]);
     }
     if (lane < 8) {
       double v;
@@ -1968,7 +1973,7 @@ struct Chain {
         case 6: v = energy; break;
         default: v = (Pr().prior_PD == 0) ? Sp->smp_s2 / (double)Pr().N : NAN; break;
       }
-      rec[lane < 7 ? lane : 7 + Pr().D] = v;
+      st_draw(&rec[lane < 7 ? lane : 7 + Pr().D], v);
     }
   }
 
@@ -2114,8 +2119,12 @@ struct Chain {
       g_add(&M.hdr[MIG_MOVES], 1);
     }
     image_out(P.mig_img + (size_t)(tt * GMAX + slot) * P.mig_img_words);
-    __threadfence();
-    if (lane == 0) g_store_rel(&M.mbox[tt * GMAX + slot], lc + 1);
+    // one wave-wide release (the L2 write-back of every lane's image stores) publishes
+    // the image to the receiver's XCD; the mailbox store itself is then relaxed
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (lane == 0)
+      __hip_atomic_store((int*)&M.mbox[tt * GMAX + slot], lc + 1, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     return true;
   }
   // the chain's LDS state at a transition boundary (scalars, vectors, sums, aux;
@@ -2243,8 +2252,11 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane) {
   AS_GLB int* box = &M.mbox[me * GMAX + c];
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   int m = 0;
+  // Poll with relaxed loads and acquire once the mailbox is set: an agent-scope acquire
+  // invalidates this XCD's L2, and up to hundreds of receivers wait at the end of a launch
+  // (each poll an invalidation would evict every tile's proposal pools on the XCD).
   for (;;) {
-    m = __builtin_amdgcn_readfirstlane(g_load_acq(box));
+    m = __builtin_amdgcn_readfirstlane(g_load(box));
     if (m != 0) break;
     if (__builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_DONE])) >= P.chains) return -1;
     if (__builtin_amdgcn_s_memrealtime() - t0 > MIG_WAIT_TICKS) {
@@ -2254,12 +2266,14 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane) {
         if (still) g_add(&M.hdr[MIG_WAITING], -1);
       }
       if (__shfl(still, 0)) return -1;
-      while ((m = __builtin_amdgcn_readfirstlane(g_load_acq(box))) == 0) __builtin_amdgcn_s_sleep(8);
+      while ((m = __builtin_amdgcn_readfirstlane(g_load(box))) == 0) __builtin_amdgcn_s_sleep(8);
       break;
     }
     __builtin_amdgcn_s_sleep(32);
   }
-  if (lane == 0) g_store_rel(box, 0);
+  // pairs with the donor's release store of the mailbox: the image is visible from here
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (lane == 0) __hip_atomic_store((int*)box, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const AS_GLB double* src =
       (const AS_GLB double*)P.mig_img + (size_t)(me * GMAX + c) * P.mig_img_words;
   AS_LDS double* dst = (AS_LDS double*)L.chain(c);
@@ -2330,7 +2344,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       const MigView M(P.mig, P.mig_tiles);
       n_active = P.G;
       __hip_atomic_store((int*)&M.load[blockIdx.x], nct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add((int*)&M.hdr[MIG_STARTED], 1, __ATOMIC_RELEASE,
+      __hip_atomic_fetch_add((int*)&M.hdr[MIG_STARTED], 1, __ATOMIC_RELAXED,   // a count: no data
                              __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -2613,7 +2627,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if (mig && lane == 0 && __builtin_amdgcn_readfirstlane(ch.Sp->state) == ST_DONE) {
           const MigView M(P.mig, P.mig_tiles);
           g_add(&M.load[blockIdx.x], -1);
-          __hip_atomic_fetch_add((int*)&M.hdr[MIG_DONE], 1, __ATOMIC_RELEASE,
+          __hip_atomic_fetch_add((int*)&M.hdr[MIG_DONE], 1, __ATOMIC_RELAXED,   // a count: no data
                                  __HIP_MEMORY_SCOPE_AGENT);
         }
        }
