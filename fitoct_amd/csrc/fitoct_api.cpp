@@ -264,7 +264,7 @@ void stage(const fitoct_problem* p, const std::vector<double>& B, const std::vec
   R* Bp = isu + n;
   for (int i = 0; i < p->N; ++i) {
     cx[i] = (R)((double)p->data_type * p->x[i]);
-    y[i] = (R)p->y[i];
+    y[i] = (R)(p->y[i] / p->uy[i]);   // y / uy: the sweep forms (y - m) / uy as one FMA
     isu[i] = (R)(1.0 / p->uy[i]);
     if (mode == MODE_POLY) {
       Bp[2 * (size_t)i] = (R)ta[2 * (size_t)i];

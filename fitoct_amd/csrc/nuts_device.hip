@@ -431,18 +431,21 @@ __device__ __forceinline__ double exp11_(double x) {
 
 // Likelihood terms of one bin given its modulation dL (shared by every mode).
 // acc: [0] sum d^2, [1] sum a, [2] sum a e, [3] sum w; returns h (adjoint seed of dL).
+// yi = y / uy is staged per bin (fitoct_api.cpp stage), so d = (y - m) / uy is one FMA,
+// and c x / L is formed once for the exponent and the theta3 weight.
 // The non-physical guard (1 + dL <= 0 -> lp = -inf) is a per-lane running min
 // (umin), applied once after the lane's bins (no per-bin selects).
 template <class R, class A, int NA>
-__device__ __forceinline__ R bin_tail(R iL, R cx, R y, R isu, R th1, R th2, A (&acc)[NA]) {
+__device__ __forceinline__ R bin_tail(R iL, R cx, R yi, R isu, R th1, R th2, A (&acc)[NA]) {
+  const R ciL = cx * iL;                                         // c x / L
   R e;                                                           // exp(-c x / L)
-  if constexpr (sizeof(R) == 8) e = exp11_(-cx * iL);
-  else e = exp_<R>(-cx * iL);
+  if constexpr (sizeof(R) == 8) e = exp11_(-ciL);
+  else e = exp_<R>(-ciL);
   const R m = fma(th2, e, th1);                                  // ui.R:88
-  const R d = (y - m) * isu;                                     // (y-m)/uy
+  const R d = fma(-m, isu, yi);                                  // (y-m)/uy
   const R a = d * isu;                                           // dlp/dm * sigma^2
   const R ae = a * e;
-  const R w = ae * cx * iL;
+  const R w = ae * ciL;
   acc[0] += (A)(d * d);
   acc[1] += (A)a;
   acc[2] += (A)ae;
@@ -450,18 +453,19 @@ __device__ __forceinline__ R bin_tail(R iL, R cx, R y, R isu, R th1, R th2, A (&
   return w * iL;                                                 // dlp/ddL / (th2 th3) * sigma^2
 }
 template <class R, class A, int NA>
-__device__ __forceinline__ R bin_core(R dL, R cx, R y, R isu, R th1, R th2, R th3, A (&acc)[NA],
+__device__ __forceinline__ R bin_core(R dL, R cx, R yi, R isu, R th1, R th2, R th3, A (&acc)[NA],
                                       R& umin) {
   const R u = R(1) + dL;
   umin = fmin(umin, u);
   const R L = th3 * u;                                           // decay length theta3*(1+dL)
   const R iL = rcp_<R>(L);
-  const R e = exp_<R>(-cx * iL);                                 // exp(-c x / L)
+  const R ciL = cx * iL;                                         // c x / L
+  const R e = exp_<R>(-ciL);                                     // exp(-c x / L)
   const R m = fma(th2, e, th1);                                  // ui.R:88
-  const R d = (y - m) * isu;                                     // (y-m)/uy
+  const R d = fma(-m, isu, yi);                                  // (y-m)/uy
   const R a = d * isu;                                           // dlp/dm * sigma^2
   const R ae = a * e;
-  const R w = ae * cx * iL;
+  const R w = ae * ciL;
   acc[0] += (A)(d * d);
   acc[1] += (A)a;
   acc[2] += (A)ae;
