@@ -77,6 +77,12 @@ enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2, FAM_MONO = 3 };
 #ifndef FITOCT_BPT16_PAIRS
 #define FITOCT_BPT16_PAIRS 0
 #endif
+// deep speculation in tiles of one chain: the helper wave does the whole bookkeeping of leaf
+// k (merge uniforms, weight, U-turn checks, merges, push, top merge) while the chain's wave
+// completes gradient k + 1
+#ifndef FITOCT_DEEP_SPEC
+#define FITOCT_DEEP_SPEC 1
+#endif
 #ifndef FITOCT_NT_DRAWS
 #define FITOCT_NT_DRAWS 1
 #endif
@@ -695,8 +701,11 @@ struct Lds {
     return (int)sizeof(ChainScalars) +
            (NVEC * VLEN + NSLOT + NAUX + max_depth * NLVL * VLEN + max_depth * WAVE) * 8;
   }
+  // tiles of one chain (deep speculation): the booked leaf's q, end-updated p, g, lp and
+  // sum r^2, handed from the chain's wave to the helper wave that books it
+  static constexpr int HX_BYTES = ((3 * VLEN + 2) * 8 + 15) / 16 * 16;
   static __host__ __device__ constexpr int bytes(int G, int max_depth) {
-    return head_bytes(G) + G * chain_bytes(max_depth);
+    return head_bytes(G) + G * chain_bytes(max_depth) + (G == 1 ? HX_BYTES : 0);
   }
   AS_LDS char* base;
   int G, cb;
@@ -712,6 +721,7 @@ struct Lds {
   __device__ AS_LDS double* sums(int c) const { return vecs(c) + NVEC * VLEN; }
   __device__ AS_LDS double* aux(int c) const { return sums(c) + NSLOT; }
   __device__ AS_LDS double* lvls(int c) const { return aux(c) + NAUX; }
+  __device__ AS_LDS double* hx() const { return (AS_LDS double*)(base + head_bytes(G) + G * cb); }
 };
 
 // The likelihood sweep of chains [cb, ce) of the tile (gradient waves only).
@@ -887,6 +897,14 @@ struct Chain {
   // the helper publishes the booked leaf's weight by writing request numbers here
   volatile AS_LDS int* help_wdone = nullptr;
   int help_want = 0;
+  // deep speculation (tiles of one chain): the helper books leaf k (deep_book) while this
+  // wave completes gradient k + 1; this wave waits for booking k (book_done >= book_want)
+  // only before it stages leaf k + 2, and reads its outcome from book_res
+  bool deep = false;
+  AS_LDS double* HX = nullptr;
+  volatile AS_LDS int* book_done = nullptr;
+  volatile AS_LDS int* book_res = nullptr;
+  int book_want = 0;
   RngKey key;
 
   __device__ Chain(KPc& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
@@ -896,6 +914,8 @@ struct Chain {
         lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
     gid = Pr().chain_offset + lc;
     helped = SPEC && !MIG && nct_ == 1;
+    deep = FITOCT_DEEP_SPEC && helped;
+    HX = L.hx();
     key = make_key(Pr().seed, (uint32_t)gid);
     if constexpr (KROW) {
       const int r = lane < NNP ? lane : 0;
@@ -1262,6 +1282,10 @@ struct Chain {
   __device__ int act_prior() {
     FITOCT_MARK(act_prior);
     const bool tree = uni(Sp->state) == ST_TREE;
+    if (deep) {   // the tree uniforms are the booking helper's (it owns the rings and Sp->leaf)
+      prior_part();
+      return A_YIELD;
+    }
     prior_and_uniforms(tree, uni(Sp->depth), uni(Sp->leaf), (uint32_t)uni(Sp->t));
     return A_YIELD;
   }
@@ -1273,7 +1297,12 @@ struct Chain {
     long long ts = stamp0();
     prior_part();
     sub(7, ts);
-    if (tree) {
+    if (tree) tree_uniforms(d, j, t);
+  }
+  // the uniforms leaf j of the subtree of depth d will consume in its merges (and the
+  // top-level merge's, for the subtree's last leaf)
+  __device__ void tree_uniforms(const int d, const int j, const uint32_t t) const {
+    {
       // Leaf j completes the merges of levels l < nm (trailing ones of j).
       // The k-th level-l merge of a subtree sits at leaf (k + 1) 2^(l+1) - 1; each
       // level keeps a ring of the uniforms of 64 consecutive merges, refilled a block
@@ -1310,6 +1339,14 @@ struct Chain {
       Sp->cur_lp = lp;
       Sp->cur_s2 = s0;
       if constexpr (spec) {   // per leaf: plain and speculative leaves leave the same state
+        if (deep) {
+          // leaf k - 1 is being booked by the helper: its outcome decides whether this leaf
+          // belongs to the trajectory, and it sets the tree coordinates this leaf continues from
+          const int w = wait_booking();
+          if (w < 0) return A_FINISH;
+          if (w == LB_END) return A_END_TREE;   // this (speculated) leaf is discarded
+          return leaf_spec(q, p, g, minv, lp, s0);
+        }
         if (helped || uni(__atomic_load_n(live, __ATOMIC_RELAXED)) <= Pr().spec_live)
           return leaf_spec(q, p, g, minv, lp, s0);
       }
@@ -1613,7 +1650,10 @@ struct Chain {
     const double e = Sp->lf_e;
     const int d = uni(Sp->depth), j = uni(Sp->leaf);
     const bool last = j == (1 << d) - 1;
-    if (last && d + 1 >= Pr().max_depth) return leaf(q, p, g, minv, cur_lp, cur_s2);
+    if (last && d + 1 >= Pr().max_depth) {   // the tree ends here at the latest: no speculation
+      if (deep) tree_uniforms(d, j, (uint32_t)uni(Sp->t));   // the helper did not draw them
+      return leaf(q, p, g, minv, cur_lp, cur_s2);
+    }
     V pe;
 #pragma unroll
     for (int s = 0; s < PPL; ++s) pe.a[s] = fma(0.5 * e, g.a[s], p.a[s]);   // end_update_p
@@ -1635,6 +1675,19 @@ struct Chain {
       en = dirn ? Sp->eps_used : -Sp->eps_used;
     }
     leapfrog_stage(qs, ps, gs, minv, en);
+    if (deep) {   // hand leaf k to the booking helper (deep_book)
+#pragma unroll
+      for (int s = 0; s < PPL; ++s) {
+        HX[idx(s)] = q.a[s];
+        HX[VLEN + idx(s)] = pe.a[s];
+        HX[2 * VLEN + idx(s)] = g.a[s];
+      }
+      if (lane == 0) {
+        HX[3 * VLEN] = cur_lp;
+        HX[3 * VLEN + 1] = cur_s2;
+      }
+      return A_SPEC_STAGED;
+    }
     // for the helper (spec_weight): the booked leaf's end-updated momentum, in CUR_G's
     // slot (while a tree grows nothing reads CUR_G; begin_subtree rewrites it)
     st(V_CUR_G, pe);   // (its lp is Sp->cur_lp, set by act_grad)
@@ -1672,6 +1725,59 @@ struct Chain {
     // without a helper, the next position's prior part follows the bookkeeping here
     if (!helped && r != LB_END) prior_and_uniforms(true, k_dn, k_jn, k_t);
     return r == LB_END ? A_SPEC_DISCARD : A_SPEC_WAIT;
+  }
+
+  // Deep speculation, run by the helper wave: the whole bookkeeping of the leaf the chain's
+  // wave handed over in HX (act_spec_book's work with the weight computed here), with the
+  // coordinates (depth, leaf, direction, step) in Sp advanced for the next leaf exactly as
+  // act_spec_book advances them -- the chain's wave reads them only after waiting for this
+  // booking.  Same operations on the same values as the plain path: same draws.
+  __device__ int deep_book() {
+    const int d = uni(Sp->depth), j = uni(Sp->leaf);
+    const uint32_t t = (uint32_t)uni(Sp->t);
+    tree_uniforms(d, j, t);
+    V q, pe, g;
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) {
+      q.a[s] = HX[idx(s)];
+      pe.a[s] = HX[VLEN + idx(s)];
+      g.a[s] = HX[2 * VLEN + idx(s)];
+    }
+    const double lp = HX[3 * VLEN], s2 = HX[3 * VLEN + 1];
+    const V minv = ld(V_MINV);
+    double h = -lp + kin(pe, minv);
+    if (isnan(h)) h = INFINITY;
+    const XF w = xf_exp(Sp->H0 - h);
+    Sp->spec_h = h;
+    Sp->spec_wm = w.m;
+    Sp->spec_we = w.e;
+    const int r = leaf_book_split(q, pe, g, minv, lp, s2);
+    if (r == LB_NEXT) {   // act_begin_subtree's bookkeeping for the subtree of depth d + 1
+      const int dirn = (uniform(key, t, TAG_DIR, (uint32_t)(d + 1), 0u) > 0.5) ? 1 : 0;
+      Sp->dir = dirn;
+      st(V_PNEAR, ld((dirn ? V_E1_Q : V_E0_Q) + 1));
+      Sp->leaf = 0;
+      if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;
+      Sp->lf_e = dirn ? Sp->eps_used : -Sp->eps_used;
+    }
+    return r;
+  }
+  // the chain's wave: wait for the booking of the previous leaf (if one is outstanding);
+  // its LB_* outcome, or -1 on a timeout (status set)
+  __device__ int wait_booking() {
+    if (book_want == 0) return LB_MID;
+    long long spins = 0;
+    while (*book_done < book_want) {
+      if (++spins > SPIN_LIMIT) {
+        Sp->status = ERR_TIMEOUT;
+        return -1;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    wave_fence();   // the booking's LDS writes are visible from here
+    const int r = uni(*book_res);
+    book_want = 0;
+    return r;
   }
 
   // run by the helper wave for the leaf being booked: its Hamiltonian and multinomial
@@ -1791,7 +1897,7 @@ struct Chain {
     }
     sub(2, ts);
     // phase B: the helper's weight of this leaf (or this wave's own, act_spec_book)
-    if (helped) {
+    if (helped && !deep) {
       long long spins = 0;
       while (*help_wdone < help_want) {
         if (++spins > SPIN_LIMIT) {
@@ -2322,7 +2428,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   // speculative leaves (P.spec, one chain per tile): the chain's NUTS wave posts a
   // request {depth, leaf, iteration} for the prior part of a speculated position; the
   // helper wave (slot 1) runs it and publishes the request number it finished
-  __shared__ int help_req, help_done, help_wdone, help_arg[3];
+  __shared__ int help_req, help_done, help_wdone, help_arg[3], help_res;
   const bool spec = SPEC;
   const bool helped = SPEC && !MIG && nct == 1;   // a spare NUTS wave helps the tile's one chain
   __shared__ int live_chains;   // chains the tile hosts (speculation policy, Chain::live)
@@ -2335,6 +2441,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     help_req = 0;
     help_done = 0;
     help_wdone = 0;
+    help_res = 0;
   }
   if (tid < GMAX) {
     grad_cnt[tid] = 0;
@@ -2460,6 +2567,16 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         spins = 0;
         seen = r;
         wave_fence();   // the request's arguments are read after its number
+        if (ch.deep) {   // book the handed-over leaf; publish its outcome, then the number
+          const int res = ch.deep_book();
+          wave_fence();
+          if (lane == 0) {
+            __atomic_store_n(&help_res, res, __ATOMIC_RELAXED);
+            wave_fence();
+            __atomic_store_n(&help_done, seen, __ATOMIC_RELAXED);
+          }
+          continue;
+        }
         ch.spec_weight();   // first what the chain's bookkeeping waits for
         wave_fence();
         if (lane == 0) __atomic_store_n(&help_wdone, seen, __ATOMIC_RELAXED);
@@ -2496,7 +2613,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
             __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
                              __ATOMIC_RELAXED);
-            if (helped) {
+            if (ch.deep) {
+              wave_fence();   // the hand-off (HX) lands before the request number
+              __atomic_store_n(&help_req, hreq + 1, __ATOMIC_RELAXED);
+            } else if (helped) {
               help_arg[0] = ch.k_dn;
               help_arg[1] = ch.k_jn;
               help_arg[2] = (int)ch.k_t;
@@ -2505,6 +2625,16 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             }
           }
           if (stamp) t_enq = (long long)__builtin_amdgcn_s_memtime();
+          if (ch.deep) {   // the helper books the leaf; this wave computes the next prior part
+            ++hreq;
+            ch.book_done = (volatile AS_LDS int*)&help_done;
+            ch.book_res = (volatile AS_LDS int*)&help_res;
+            ch.book_want = hreq;
+            ++epoch;
+            a = Ch::A_PRIOR;
+            in_sweep = true;
+            continue;
+          }
           if (helped) {
             ++hreq;
             ch.help_wdone = (volatile AS_LDS int*)&help_wdone;
