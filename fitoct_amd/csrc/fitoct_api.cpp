@@ -945,6 +945,7 @@ int32_t fitoct_plan_wait(fitoct_plan* pl) {
       double subt[12] = {0}, wb[8] = {0};
       for (int t = 0; t < pl->tiles; ++t) {
         for (int k = 0; k < 8; ++k) subt[k] += h[(size_t)NSTAMP * t + 48 + k];
+        for (int k = 0; k < 4; ++k) subt[8 + k] += h[(size_t)NSTAMP * t + 68 + k];
         for (int k = 0; k < 8; ++k) wb[k] += h[(size_t)NSTAMP * t + 56 + k];
       }
       fprintf(stderr, "[fitoct stamps] gradient-wave busy per sweep by wave:");

@@ -1766,6 +1766,7 @@ struct Chain {
   // its LB_* outcome, or -1 on a timeout (status set)
   __device__ int wait_booking() {
     if (book_want == 0) return LB_MID;
+    long long ts = stamp0();   // profiling build: sub-stamp 8 = this wave's stall on the booking
     long long spins = 0;
     while (*book_done < book_want) {
       if (++spins > SPIN_LIMIT) {
@@ -1775,6 +1776,7 @@ struct Chain {
       __builtin_amdgcn_s_sleep(1);
     }
     wave_fence();   // the booking's LDS writes are visible from here
+    sub(8, ts);
     const int r = uni(*book_res);
     book_want = 0;
     return r;
@@ -2799,6 +2801,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         o[22 + k] = L.cs(0).prof[1][k];
       }
       for (int k = 0; k < 8; ++k) o[48 + k] = L.cs(0).prof[0][20 + k];
+      for (int k = 0; k < 4; ++k) o[68 + k] = L.cs(0).prof[0][28 + k];
     }
   }
 }
