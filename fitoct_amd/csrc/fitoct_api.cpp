@@ -699,7 +699,7 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   pl->draws_bytes = sizeof(double) * (size_t)C * k.iters_saved * k.ncols;
   const int vlen = WAVE * pl->ppl;
   auto setup = [&]() -> int {
-    HIP_TRY(hipMalloc(&pl->d_stack, sizeof(double) * (size_t)C * (cfg->max_treedepth + 1) * 3 * vlen));
+    HIP_TRY(hipMalloc(&pl->d_stack, sizeof(double) * (size_t)C * (cfg->max_treedepth + 1) * POOL_VECS * vlen));
     HIP_TRY(hipMalloc(&pl->d_fin, sizeof(double) * (size_t)C * (1 + 2 * D)));
     HIP_TRY(hipMalloc(&pl->d_status, sizeof(int) * C));
     HIP_TRY(hipMalloc(&pl->d_leap, sizeof(long long) * C));

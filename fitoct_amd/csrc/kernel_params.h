@@ -18,7 +18,7 @@ constexpr int GMAX = NW - NGW;    // NUTS waves (4..7), one chain each: max chai
 constexpr int MAXDEPTH = 16;      // hard cap on max_treedepth
 constexpr int NSLOT = 32;         // reduced sums per chain (4 + NNP <= 32)
 constexpr int MPW = 32;           // model-parameter words per chain (theta[3], pad, yGP[NNP])
-constexpr int NSTK = 6;           // vectors per tree level in the global stack
+constexpr int POOL_VECS = 2;      // vectors per proposal-pool slot in HBM (q, grad)
 constexpr int KMAX = 24;          // max GP control points (K^-1 tile in LDS)
 constexpr int NSTAMP = 72;        // diagnostic stamps per tile (FITOCT_STAMPS)
 
@@ -84,7 +84,7 @@ struct KParams {
   // ---- outputs ----
   double* draws;            // [chains][iters_saved][ncols]
   int ncols, iters_saved;
-  double* stack;            // [chains][max_depth][NSTK][vlen]
+  double* stack;            // proposal pool [chains][max_depth + 1][POOL_VECS][vlen]
   double* fin_eps;          // [chains]
   double* fin_minv;         // [chains][D]
   double* fin_q;            // [chains][D]

@@ -37,7 +37,7 @@
 //     log-Jacobians, and advances the chain's state machine.  Stan's recursive
 //     build_tree is replayed iteratively, one leaf per step: the U-turn records
 //     (p_beg, p_end, rho) of each tree level live in LDS, the multinomial
-//     proposals (q, p, grad) in a per-chain HBM pool addressed by slot index, so
+//     proposals (q, grad; the momentum only as its energy) in a per-chain HBM pool addressed by slot index, so
 //     a proposal is written once when its leaf is pushed and read only when it
 //     becomes the sample.  Wave reductions are DPP/permlane butterflies.
 //   * workgroups communicate only to hand whole chains between tiles at transition
@@ -111,7 +111,7 @@ enum VecId : int {
   V_CUR_Q, V_CUR_P, V_CUR_G,
   V_E0_Q, V_E0_P, V_E0_G,      // backward end of the trajectory
   V_E1_Q, V_E1_P, V_E1_G,      // forward end
-  V_SMP_Q, V_SMP_P, V_SMP_G,   // z_sample
+  V_SMP_Q, V_SMP_G,            // z_sample (its momentum enters only the energy: smp_h)
   V_MINV, V_WF_M, V_WF_M2,     // metric + Welford
   V_RHO, V_PNEAR,              // trajectory momentum sum, near end of old trajectory
   V_QS, V_QE,                  // staged q and its constrained values (exp on positive params)
@@ -120,8 +120,10 @@ enum VecId : int {
 };
 // U-turn record of one tree level (LDS)
 enum LvlId : int { K_PBEG = 0, K_PEND = 1, K_RHO = 2, NLVL = 3 };
-// proposal pool slot (HBM)
-enum PoolId : int { P_Q = 0, P_P = 1, P_G = 2, NPOOL = 3 };
+// proposal pool slot (HBM): q and g of a candidate sample.  Its momentum is dead once it is
+// a candidate (the next transition draws a fresh one) except in the energy__ diagnostic,
+// H(z_sample), which is the candidate leaf's own Hamiltonian h: kept as a scalar (pool_h)
+enum PoolId : int { P_Q = 0, P_G = 1, NPOOL = POOL_VECS };
 constexpr int NAUX = 96;   // per chain: yGP[32] | horseshoe lambda_j*tau [32] | FW_j [32]
 
 struct ChainScalars {
@@ -140,6 +142,8 @@ struct ChainScalars {
   double pool_lp[MAXDEPTH + 1], pool_s2[MAXDEPTH + 1];
   long long leapfrogs;
   double spec_h;
+  // Hamiltonian -lp + K(p) of each pool candidate and of the sample (energy__)
+  double pool_h[MAXDEPTH + 1], smp_h;
   long long prof[2][32];   // diagnostic build: cycles and calls per action
 };
 static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
@@ -202,11 +206,13 @@ constexpr int DPP_QREV = 0x1B;         // quad_perm(3,2,1,0): flip bits 0,1
 constexpr int DPP_HALF_MIRROR = 0x141; // lane i <-> 7-i within 8: flip bits 0..2
 constexpr int DPP_MIRROR = 0x140;      // lane i <-> 15-i within 16: flip bits 0..3
 
+// (bound_ctrl: a disabled source lane reads 0, as the zero 'old' operand of update_dpp
+// gave, without a v_mov of that zero before every DPP move)
 template <int CTRL>
 __device__ __forceinline__ double dpp(double x) {
   const uint64_t u = __builtin_bit_cast(uint64_t, x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
   return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 // v_readlane of a double (lane index wave-uniform)
@@ -1557,8 +1563,8 @@ struct Chain {
     Sp->eps_used = Sp->eps;
     const V minv = ld(V_MINV);
     const V p = momentum(TAG_MOM, (uint32_t)uni(Sp->t), 0u, minv);
-    st(V_SMP_P, p);
     Sp->H0 = -Sp->smp_lp + kin(p, minv);
+    Sp->smp_h = Sp->H0;   // energy__ if no leaf replaces the initial point
     const V q = ld(V_SMP_Q), g = ld(V_SMP_G);
     st(V_E0_Q, q); st(V_E0_P, p); st(V_E0_G, g);
     st(V_E1_Q, q); st(V_E1_P, p); st(V_E1_G, g);
@@ -1596,23 +1602,22 @@ struct Chain {
 
   // proposal pool: at most max_depth + 1 live slots (stack records + the running
   // subtree).  `used` is the slot bitmask, kept in registers by the caller.
-  __device__ int pool_put(unsigned& used, const V& q, const V& p, const V& g, double lp,
-                          double s2) const {
+  __device__ int pool_put(unsigned& used, const V& q, const V& g, double lp, double s2,
+                          double h) const {
     const int sl = __builtin_ctz(~used);
     used |= 1u << sl;
     AS_GLB double* dq = pslot(sl, P_Q);
-    AS_GLB double* dp = pslot(sl, P_P);
     AS_GLB double* dg = pslot(sl, P_G);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {   // HBM stores, never waited on; D lanes only (the
-      if (ok(s)) {                    // padding lanes of q, p, g are 0: top_merge reads 0)
+      if (ok(s)) {                    // padding lanes of q, g are 0: top_merge reads 0)
         dq[idx(s)] = q.a[s];
-        dp[idx(s)] = p.a[s];
         dg[idx(s)] = g.a[s];
       }
     }
     Sp->pool_lp[sl] = lp;
     Sp->pool_s2[sl] = s2;
+    Sp->pool_h[sl] = h;
     return sl;
   }
 
@@ -1800,8 +1805,9 @@ struct Chain {
   // of the sample (u_top drawn by act_prior) and the trajectory weight.  Shared by
   // leaf_book and leaf_book_split.
   __device__ __forceinline__ void top_merge(const V& q, const V& p, const V& g, const double cur_lp,
-                                            const double cur_s2, const XF Tw, const int Tprop,
-                                            unsigned used, const int dir, const int d) const {
+                                            const double cur_s2, const double h, const XF Tw,
+                                            const int Tprop, unsigned used, const int dir,
+                                            const int d) const {
     const XF Ww{Sp->lsw_m, Sp->lsw_e};
     const double u_top = Sp->u_top;
     const int eq = dir ? V_E1_Q : V_E0_Q;
@@ -1815,26 +1821,24 @@ struct Chain {
     if (take) {
       if (Tprop < 0) {
         st(V_SMP_Q, q);
-        st(V_SMP_P, p);
         st(V_SMP_G, g);
         Sp->smp_lp = cur_lp;
         Sp->smp_s2 = cur_s2;
+        Sp->smp_h = h;
       } else {
         const AS_GLB double* sq = pslot(Tprop, P_Q);
-        const AS_GLB double* sp = pslot(Tprop, P_P);
         const AS_GLB double* sg = pslot(Tprop, P_G);
-        V q2, p2, g2;
+        V q2, g2;
 #pragma unroll
         for (int s = 0; s < PPL; ++s) {
           q2.a[s] = ok(s) ? sq[idx(s)] : 0.0;
-          p2.a[s] = ok(s) ? sp[idx(s)] : 0.0;
           g2.a[s] = ok(s) ? sg[idx(s)] : 0.0;
         }
         st(V_SMP_Q, q2);
-        st(V_SMP_P, p2);
         st(V_SMP_G, g2);
         Sp->smp_lp = Sp->pool_lp[Tprop];
         Sp->smp_s2 = Sp->pool_s2[Tprop];
+        Sp->smp_h = Sp->pool_h[Tprop];
       }
     }
     if (Tprop >= 0) used &= ~(1u << Tprop);
@@ -1946,7 +1950,7 @@ struct Chain {
       lst(nm, K_RHO, Trho);
       Sp->st_w_m[nm] = Tw.m;
       Sp->st_w_e[nm] = Tw.e;
-      Sp->st_prop[nm] = (Tprop < 0) ? pool_put(used, q, p, g, cur_lp, cur_s2) : Tprop;
+      Sp->st_prop[nm] = (Tprop < 0) ? pool_put(used, q, g, cur_lp, cur_s2, h) : Tprop;
     }
     sub(0, ts);
     if (!last) {
@@ -1955,7 +1959,7 @@ struct Chain {
       return LB_MID;
     }
     // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
-    top_merge(q, p, g, cur_lp, cur_s2, Tw, Tprop, used, dir, d);
+    top_merge(q, p, g, cur_lp, cur_s2, h, Tw, Tprop, used, dir, d);
     st(V_RHO, rtot);
     sub(3, ts);
     if (!persist || d + 1 >= Pr().max_depth) return LB_END;
@@ -1998,7 +2002,7 @@ struct Chain {
         lst(l, K_RHO, Trho);
         Sp->st_w_m[l] = Tw.m;
         Sp->st_w_e[l] = Tw.e;
-        Sp->st_prop[l] = (Tprop < 0) ? pool_put(used, q, p, g, cur_lp, cur_s2) : Tprop;
+        Sp->st_prop[l] = (Tprop < 0) ? pool_put(used, q, g, cur_lp, cur_s2, h) : Tprop;
         break;
       }
       // merge init I = level l with final T (base_nuts::build_tree at depth l+1)
@@ -2038,7 +2042,7 @@ struct Chain {
     }
     // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
     const int dir = uni(Sp->dir);
-    top_merge(q, p, g, cur_lp, cur_s2, Tw, Tprop, used, dir, d);
+    top_merge(q, p, g, cur_lp, cur_s2, h, Tw, Tprop, used, dir, d);
     const V far = ld(dir ? V_E0_P : V_E1_P), near = ld(V_PNEAR), rho = ld(V_RHO);
     V rtot, rx, ry;
 #pragma unroll
@@ -2092,8 +2096,9 @@ struct Chain {
   __device__ int act_end_tree() {
     FITOCT_MARK(act_end_tree);
     const double accept = Sp->sum_metro / (double)Sp->n_leapfrog;
-    const V minv = ld(V_MINV);
-    const double energy = -Sp->smp_lp + kin(ld(V_SMP_P), minv);
+    // energy__ = H(z_sample) (base_nuts::transition), the sample leaf's own -lp + K(p):
+    // the same operations on the same values as -smp_lp + kin(p_sample)
+    const double energy = Sp->smp_h;
     write_draw(accept, energy);
     Sp->leapfrogs += Sp->n_leapfrog;
     if (uni(Sp->t) < Pr().warmup && Pr().adapt) {
