@@ -288,6 +288,21 @@ __device__ __forceinline__ void wave_sum_n(double (&x)[N]) {
 // |r| <= ln2/2, n = round(x log2 e) from the 1.5*2^52 shifter fed straight to
 // v_ldexp_f64 (<= 2 ulp from the library exp, scripts/micro/acc.hip; no special
 // cases: x is clamped to [-746, 710], where exp is 0 / inf either way).
+// v_fma_f64 with all three operands in VGPRs.  In the sampler's code the compiler keeps
+// fexp's coefficients in VGPRs (its SGPRs are spent) and forms p * r + c as a copy of c into
+// the destination plus a v_fmac_f64: two VALU instructions per Horner step.  Same operation.
+__device__ __forceinline__ double fma_v(double a, double b, double c) {
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+template <bool V3>
+__device__ __forceinline__ double fmac3(double a, double b, double c) {
+  if constexpr (V3) return fma_v(a, b, c);
+  else return fma(a, b, c);
+}
+// V3: Horner steps as fma_v (the samplers where that form compiles without spills, Chain::FV3)
+template <bool V3 = false>
 __device__ __forceinline__ double fexp(double x) {
   x = fmin(fmax(x, -746.0), 710.0);
   const double SH = 6755399441055744.0;   // 1.5 * 2^52
@@ -297,18 +312,18 @@ __device__ __forceinline__ double fexp(double x) {
   double r = fma(-n, 6.93147180369123816490e-01, x);
   r = fma(-n, 1.90821492927058770002e-10, r);
   double p = 2.08767569878680989792e-09;   // 1/12!
-  p = fma(p, r, 2.50521083854417187751e-08);
-  p = fma(p, r, 2.75573192239858906526e-07);
-  p = fma(p, r, 2.75573192239858906526e-06);
-  p = fma(p, r, 2.48015873015873015873e-05);
-  p = fma(p, r, 1.98412698412698412698e-04);
-  p = fma(p, r, 1.38888888888888888889e-03);
-  p = fma(p, r, 8.33333333333333333333e-03);
-  p = fma(p, r, 4.16666666666666666667e-02);
-  p = fma(p, r, 1.66666666666666666667e-01);
-  p = fma(p, r, 0.5);
-  p = fma(p, r, 1.0);
-  p = fma(p, r, 1.0);
+  p = fmac3<V3>(p, r, 2.50521083854417187751e-08);
+  p = fmac3<V3>(p, r, 2.75573192239858906526e-07);
+  p = fmac3<V3>(p, r, 2.75573192239858906526e-06);
+  p = fmac3<V3>(p, r, 2.48015873015873015873e-05);
+  p = fmac3<V3>(p, r, 1.98412698412698412698e-04);
+  p = fmac3<V3>(p, r, 1.38888888888888888889e-03);
+  p = fmac3<V3>(p, r, 8.33333333333333333333e-03);
+  p = fmac3<V3>(p, r, 4.16666666666666666667e-02);
+  p = fmac3<V3>(p, r, 1.66666666666666666667e-01);
+  p = fmac3<V3>(p, r, 0.5);
+  p = fmac3<V3>(p, r, 1.0);
+  p = fmac3<V3>(p, r, 1.0);
   return ldexp(p, ni);
 }
 // 1/x to <= 1 ulp: v_rcp_f64 and one Newton step (x finite, nonzero)
@@ -331,8 +346,9 @@ __device__ __forceinline__ XF xf_norm(double m, int e) {
   const double f = frexp(m, &k);
   return XF{f, f == 0.0 ? 0 : e + k};
 }
+template <bool V3 = false>
 __device__ __forceinline__ XF xf_exp(double x) {   // exp(x), x <= +inf; -inf -> 0
-  if (x > -700.0 && x < 700.0) return xf_norm(fexp(x), 0);
+  if (x > -700.0 && x < 700.0) return xf_norm(fexp<V3>(x), 0);
   // above 1e8 (an energy drop no trajectory of a finite start reaches) the weight
   // saturates: the exponent stays within int, and so does the exponent difference of
   // two weights in xf_u_below (>= -1.45e9 - 1.45e8)
@@ -341,7 +357,7 @@ __device__ __forceinline__ XF xf_exp(double x) {   // exp(x), x <= +inf; -inf ->
   // an int; the weight is 0 to every digit the merges can resolve
   if (!(x > -1.0e9)) return XF{0.0, 0};
   const double k = floor(x * 1.4426950408889634);   // log2(e)
-  return xf_norm(fexp(fma(-k, 0.6931471805599453, x)), (int)k);
+  return xf_norm(fexp<V3>(fma(-k, 0.6931471805599453, x)), (int)k);
 }
 __device__ __forceinline__ XF xf_add(XF a, XF b) {
   if (a.m == 0.0) return b;
@@ -879,6 +895,10 @@ struct Chain {
   // of every leaf (write_mp, finish_grad): same arithmetic, no LDS reads on the
   // NUTS wave's critical path (configs 2 / 5 +2 %).  Not at NNP = 24 (it would spill).
   static constexpr bool KROW = NNP <= 16;
+  // fexp's Horner steps as three-VGPR FMAs (fma_v) in the non-migrating samplers: bitwise
+  // the same, configs 2 / 5 +2 / +0.6 %.  The migrating samplers then spill a VGPR (the
+  // headline horseshoe one loses 2.2 %, profiles/r03_ab_fmav.txt): they keep the compiler's form
+  static constexpr bool FV3 = !MIG;
   double krow[KROW ? NNP : 1];
   const AS_LDS double* bv;
   int lane, slot, lc, gid, nct;
@@ -1035,14 +1055,14 @@ struct Chain {
       const double a1 = qs[5 + Nn + jl], a2 = qs[5 + 2 * Nn + jl];
       const double g1 = qs[3 + Nn], g2 = qs[4 + Nn];
       u = qs[3 + jl];
-      hl = fexp(fma(0.5, a2, a1) + fma(0.5, g2, g1));
+      hl = fexp<FV3>(fma(0.5, a2, a1) + fma(0.5, g2, g1));
     } else {
       u = qs[3 + jl];
     }
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
-      const double ev = (k < D && is_log(k)) ? fexp(q.a[s]) : q.a[s];
+      const double ev = (k < D && is_log(k)) ? fexp<FV3>(q.a[s]) : q.a[s];
       qe[k] = ev;
       if (s == 0 && lane < 3) MP[lane] = ev;   // theta for the gradient waves
     }
@@ -1752,7 +1772,7 @@ struct Chain {
     const V minv = ld(V_MINV);
     double h = -lp + kin(pe, minv);
     if (isnan(h)) h = INFINITY;
-    const XF w = xf_exp(Sp->H0 - h);
+    const XF w = xf_exp<FV3>(Sp->H0 - h);
     Sp->spec_h = h;
     Sp->spec_wm = w.m;
     Sp->spec_we = w.e;
@@ -1793,7 +1813,7 @@ struct Chain {
     const V pe = ld(V_CUR_G), minv = ld(V_MINV);   // leaf_spec staged the momentum there
     double h = -Sp->cur_lp + kin(pe, minv);
     if (isnan(h)) h = INFINITY;
-    const XF w = xf_exp(Sp->H0 - h);
+    const XF w = xf_exp<FV3>(Sp->H0 - h);
     Sp->spec_h = h;
     Sp->spec_wm = w.m;
     Sp->spec_we = w.e;
@@ -1983,7 +2003,7 @@ struct Chain {
     if (isnan(h)) h = INFINITY;
     sub(0, ts);
     const double wl = H0 - h;
-    const XF wleaf = xf_exp(wl);
+    const XF wleaf = xf_exp<FV3>(wl);
     Sp->sum_metro = sum_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
     sub(1, ts);
     if (h - H0 > 1000.0) {   // divergent: the transition ends here
