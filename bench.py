@@ -278,6 +278,8 @@ def main():
     for w in range(args.warmup):
         with plan_for(-1 - w) as pl:
             run_step(pl)
+        if rank == 0:   # progress on stderr (a long run stays visibly alive; stdout is the line)
+            print(f"[bench] warmup step {w + 1}/{args.warmup} done", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
 
     plans = [plan_for(s) for s in range(args.steps)]     # inputs staged in HBM up front
@@ -286,9 +288,12 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kernel_ms = []
-    for pl in plans:
+    for i, pl in enumerate(plans):
         run_step(pl)
         kernel_ms.append(pl.download(with_draws=False).kernel_ms)
+        if rank == 0:
+            print(f"[bench] step {i + 1}/{args.steps}: kernel {kernel_ms[-1]:.1f} ms",
+                  file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
