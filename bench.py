@@ -207,6 +207,18 @@ def main():
     ap.add_argument("--no-hard", action="store_true",
                     help="skip the hard-geometry sub-line (one extra config-3 step at "
                          "adapt_delta 0.99, max_treedepth 12; N = 1 only)")
+    ap.add_argument("--devices", type=int, default=0,
+                    help="the single-process route: one plan over the C ABI's device list "
+                         "(fitoct_config.devices, what R's fitExpGP(n_gpus = N) drives through "
+                         ".Call; FitOCT.R:110, server.R:408) on N GPUs, the config's chains per "
+                         "GPU, the in-process xGMI gather into one device buffer inside the "
+                         "step; run without torchrun (--gpus 1).  0 / 1: one device")
+    ap.add_argument("--device-ids", type=str, default="",
+                    help="explicit ordinals for --devices, e.g. 0,0 rehearses two entries on "
+                         "one GPU")
+    ap.add_argument("--no-device-list", action="store_true",
+                    help="under torchrun (N > 1): skip the device-list sub-line that rank 0 "
+                         "times over all N GPUs after the per-rank steps")
     args = ap.parse_args()
     if args.config == 5 and args.iters == f"{WARMUP_IT},{SAMPLES}":
         args.iters = "%d,%d" % CONFIGS[5]["iters"]
@@ -225,6 +237,17 @@ def main():
     backend = os.environ.get("FITOCT_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
     local = local % max(ndev, 1)
+    dev_list = ()
+    if args.devices > 1 or args.device_ids:
+        if world > 1:
+            raise SystemExit("--devices is the single-process route: run it without torchrun")
+        dev_list = (tuple(int(v) for v in args.device_ids.split(",")) if args.device_ids
+                    else tuple(range(args.devices)))
+        if args.devices > 1 and len(dev_list) != args.devices:
+            raise SystemExit(f"--devices {args.devices} but --device-ids lists {len(dev_list)}")
+        if max(dev_list) >= ndev:
+            raise SystemExit(f"--devices: device {max(dev_list)} of {ndev} visible")
+
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -237,7 +260,8 @@ def main():
     cdev = dev if backend == "nccl" else torch.device("cpu")   # where collectives run
 
     if args.config == 5:
-        return bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it)
+        return bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it,
+                           dev_list)
 
     from fitoct_amd import Plan
     from fitoct_amd.api import SamplerConfig  # noqa: F401  (import check)
@@ -247,11 +271,14 @@ def main():
     prob = make_problem(conf["prior"], N_bins)
     C = args.chains or conf["chains"]
     offset = rank * C
+    n_units = len(dev_list) or world      # GPUs the job's chains span (ranks or list entries)
+    C_plan = C * max(1, len(dev_list))    # chains of this process's plan
 
     def plan_for(step):
-        cfg = make_config(1000 + step, C, offset, local, W_it, S_it, args.adapt_delta,
+        cfg = make_config(1000 + step, C_plan, offset, local, W_it, S_it, args.adapt_delta,
                           args.max_treedepth)
         cfg.precision = args.precision
+        cfg.devices = dev_list
         return Plan(prob, cfg)
 
     stream = torch.cuda.current_stream(dev)
@@ -268,7 +295,9 @@ def main():
                 bufs["gather"] = [torch.empty(key // 8, dtype=torch.float64, device=cdev)
                                   for _ in range(world)]
         buf = bufs[key]
-        pl.run(d_draws=buf.data_ptr(), stream=stream.cuda_stream)
+        # a device list runs each GPU on a private stream of the library (stream = NULL),
+        # and gathers every block into `buf` (on this process's device) before returning
+        pl.run(d_draws=buf.data_ptr(), stream=0 if dev_list else stream.cuda_stream)
         if world > 1:   # one gather of every rank's draws to rank 0 (RCCL over xGMI)
             src = buf if backend == "nccl" else buf.cpu()
             dist.gather(src, gather_list=bufs.get("gather") if rank == 0 else None, dst=0)
@@ -313,7 +342,7 @@ def main():
         lf_all = np.array(lf_steps, dtype=np.float64)
 
     ms_per_step = wall * 1e3 / args.steps
-    draws_step = world * C * S_it
+    draws_step = world * C_plan * S_it
     value = draws_step / (ms_per_step / 1e3)
 
     # convergence of the last step (rank 0's chains): split R-hat over parameters
@@ -321,7 +350,7 @@ def main():
     cols = prob.column_names()
     W_saved = outs[-1].warmup_saved
     conv = convergence(last, W_saved, cols)
-    lf_per_draw = float(np.mean(lf_steps)) / (C * (W_it + S_it))
+    lf_per_draw = float(np.mean(lf_steps)) / (C_plan * (W_it + S_it))
 
     workload = (f"fitExpGP+{conf['prior']} N={N_bins} Nn={NN} {C} chains/GPU "
                 f"W={W_it} S={S_it} treedepth<={args.max_treedepth}"
@@ -344,15 +373,19 @@ def main():
     line = {
         "metric": ("posterior draws/sec (all chains), ExpGP N=2048 @ 1024 chains; R-hat"
                    if args.config == 3 else f"posterior draws/sec (all chains), config {args.config}"),
-        "value": round(value, 2), "unit": "draws/s", "n_gpus": world, "steps": args.steps,
+        "value": round(value, 2), "unit": "draws/s", "n_gpus": n_units, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64" if args.precision == "f64"
         else "f32-sweep/f64-state", "data": "synthetic (restated synthData.R sincExp decay)",
         "config": {"workload": workload, "prior": conf["prior"], "N": N_bins, "Nn": NN,
-                   "chains_per_gpu": C, "global_chains": world * C, "warmup_iters": W_it,
+                   "chains_per_gpu": C, "global_chains": n_units * C, "warmup_iters": W_it,
                    "samples": S_it, "adapt_delta": args.adapt_delta,
                    "max_treedepth": args.max_treedepth,
-                   "parallelism": f"chains sharded over {world} GPU(s)"},
+                   "parallelism": (f"chains sharded over {world} GPU(s)" if not dev_list else
+                                   f"device list {list(dev_list)} in one process "
+                                   "(fitoct_config.devices: R fitExpGP(n_gpus) route)"),
+                   "route": ("device-list" if dev_list else
+                             "torch.distributed" if world > 1 else "single-device")},
         **conv,
         "gradients_per_iteration": round(lf_per_draw, 1),
         # sampling phase alone: the kernel is gradient-bound, so its time is
@@ -362,7 +395,7 @@ def main():
         "total_gradients_per_step": float(lf_all.mean()),
         "roofline": roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and n_units == 1 and not args.no_cpu:
         cb = cpu_baseline(prob, float(np.mean(lf_steps)), C * S_it, args.adapt_delta,
                           args.max_treedepth)
         o_means = cb.pop("means")
@@ -376,16 +409,73 @@ def main():
         line["posterior_mean_relerr_vs_cpu"] = rel
     for pl in plans:
         pl.close()
-    if (args.config == 3 and world == 1 and not args.no_hard and args.adapt_delta == 0.8
+    bufs.clear()
+    if (args.config == 3 and n_units == 1 and not args.no_hard and args.adapt_delta == 0.8
             and args.chains == 0 and (W_it, S_it) == (WARMUP_IT, SAMPLES)):
         line["hard_geometry"] = hard_geometry(prob, C, local, dev, W_it, S_it, cols,
                                               line.get("cpu_baseline"),
                                               o_means if "cpu_baseline" in line else None)
+    if world > 1 and not args.no_device_list:
+        # the route R takes (.Call -> fitoct_config.devices), timed on the same node: rank 0
+        # alone drives every GPU of the job from one process while the other ranks wait on
+        # a host (gloo) barrier, so no collective kernel occupies their GPUs meanwhile
+        hb = dist.new_group(backend="gloo")
+        dist.barrier(group=hb)
+        if rank == 0:
+            line["device_list"] = device_list_leg(
+                lambda step, devs: Plan(prob, _dl_config(args, C * len(devs), W_it, S_it,
+                                                         step, devs)),
+                _dl_devices(world), C * S_it, dev, f_grad(N_bins, NN))
+        dist.barrier(group=hb)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _dl_devices(world):
+    """GPUs of the device-list sub-line: the job's, 0..world-1 (one node, one rank per GPU).
+    FITOCT_BENCH_DEVICE_LIST=0,0 rehearses it with ranks sharing one GPU (gloo backend)."""
+    env = os.environ.get("FITOCT_BENCH_DEVICE_LIST", "")
+    return tuple(int(v) for v in env.split(",") if v) or tuple(range(world))
+
+
+def _dl_config(args, chains, W_it, S_it, step, devs):
+    cfg = make_config(1000 + step, chains, 0, devs[0], W_it, S_it, args.adapt_delta,
+                      args.max_treedepth)
+    cfg.devices = devs
+    return cfg
+
+
+def device_list_leg(make, devs, draws_per_gpu, dev, flop_per_grad, is_batch=False):
+    """One step of the single-process route over `devs` (the C ABI's device list:
+    one host thread per GPU inside libfitoct, blocks gathered over xGMI into one
+    buffer on `dev` before the call returns), timed like a headline step: the
+    plan (basis, staging) is created before the timer.  `make(step, devs)` builds
+    the plan or batch (seed 1000 + step, the first timed step's seed)."""
+    import torch
+    with make(0, devs) as pl:
+        buf = torch.empty(pl.info["draws_bytes"] // 8, dtype=torch.float64, device=dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pl.run(d_draws=buf.data_ptr())
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        o = pl.download(0, with_draws=False) if is_batch else pl.download(with_draws=False)
+        kms, lf = o.kernel_ms, (None if is_batch else o.total_leapfrogs)
+    res = {"route": "fitoct_config.devices (one process, one host thread per GPU; "
+                    "R fitExpGP(n_gpus) via .Call)",
+           "devices": list(devs), "value": round(len(devs) * draws_per_gpu / wall, 2),
+           "unit": "draws/s", "ms_per_step": round(wall * 1e3, 2),
+           "kernel_ms_max_over_devices": round(kms, 2), "steps": 1,
+           "gather": "in-process hipMemcpyPeer of every block into one buffer on GPU "
+                     f"{dev.index}, inside the step"}
+    if lf:
+        res["gradients_per_launch"] = lf
+        res["roofline_frac_per_gpu"] = round(flop_per_grad * lf / len(devs) / (kms / 1e3)
+                                             / 1e12 / FP64_VALU_PEAK_TF, 4)
+    return res
 
 
 def hard_geometry(prob, C, local, dev, W_it, S_it, cols, cpu, o_means):
@@ -444,9 +534,10 @@ def hard_geometry(prob, C, local, dev, W_it, S_it, cols, cpu, o_means):
     return res
 
 
-def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
+def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it, dev_list=()):
     """Config 5 (FitOCT.R batch mode): this rank's files in ONE batched launch
-    (fitoct_batch_*); one gather of every rank's draws to rank 0 inside the step."""
+    (fitoct_batch_*); one gather of every rank's draws to rank 0 inside the step.
+    With ``--devices N`` (one process) the batch runs over the C ABI's device list."""
     import torch
     from fitoct_amd import Batch, ExpGPProblem, SamplerConfig
     from fitoct_amd.stanfit import split_rhat_ess
@@ -456,21 +547,26 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
     t0, S0 = default_prior()
     from fitoct_amd.distributed import shard_range
     f_off, f_cnt = shard_range(conf["files"], world, rank)   # contiguous file blocks
-    files = list(range(f_off, f_off + f_cnt))
-    probs = []
-    for f in files:
-        d = synth_decay(conf["N"], MODULATIONS[f % 4], 1234 + f)
-        probs.append(ExpGPProblem(d["x"], d["y"], d["uy"], dataType=2, Nn=NN,
-                                  gridType="extremal", theta0=t0, Sigma0=S0,
-                                  prior_type=conf["prior"]))
-    C = args.chains or conf["chains"]
 
-    def batch_for(step):
+    def file_problems(first, count):
+        out = []
+        for f in range(first, first + count):
+            d = synth_decay(conf["N"], MODULATIONS[f % 4], 1234 + f)
+            out.append(ExpGPProblem(d["x"], d["y"], d["uy"], dataType=2, Nn=NN,
+                                    gridType="extremal", theta0=t0, Sigma0=S0,
+                                    prior_type=conf["prior"]))
+        return out
+    files = list(range(f_off, f_off + f_cnt))
+    probs = file_problems(f_off, f_cnt)
+    C = args.chains or conf["chains"]
+    n_units = len(dev_list) or world
+
+    def batch_for(step, ps=probs, first=f_off, devs=dev_list):
         # file f's chains are global chains f*C + c (fitoct_amd.distributed.sample_batch_sharded)
         cfg = SamplerConfig(chains=C, warmup=W_it, samples=S_it, seed=2000 + step,
                             adapt_delta=0.8, max_treedepth=10, device=local,
-                            chain_offset=f_off * C)
-        return Batch(probs, cfg)
+                            chain_offset=first * C, devices=devs)
+        return Batch(ps, cfg)
 
     stream = torch.cuda.current_stream(dev)
     bufs = {}
@@ -480,7 +576,7 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
         if key not in bufs:
             bufs[key] = torch.empty(key // 8, dtype=torch.float64, device=dev)
         buf = bufs[key]
-        b.run(d_draws=buf.data_ptr(), stream=stream.cuda_stream)
+        b.run(d_draws=buf.data_ptr(), stream=0 if dev_list else stream.cuda_stream)
         if world > 1:   # ragged file counts per rank: all_gather of sizes, then gather
             src = buf if backend == "nccl" else buf.cpu()
             n = torch.tensor([src.numel()], dtype=torch.int64, device=cdev)
@@ -526,14 +622,18 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
     line = {
         "metric": "posterior draws/sec (all chains), config 5 (FitOCT.R batch mode)",
         "value": round(draws_step / (ms_per_step / 1e3), 2), "unit": "draws/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "n_gpus": n_units, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (restated synthData.R, 4 modulations cycled over files)",
         "config": {"workload": f"FitOCT.R batch: {conf['files']} files x {C} chains, "
                                f"fitExpGP+{conf['prior']} N={conf['N']} Nn={NN} W={W_it} S={S_it}",
                    "files": conf["files"], "files_this_rank": len(files), "chains_per_file": C,
-                   "parallelism": f"files in contiguous blocks over {world} GPU(s), one launch per GPU"},
+                   "parallelism": (f"files in contiguous blocks over {n_units} GPU(s), one "
+                                   "launch per GPU" + (f" (device list {list(dev_list)}, one "
+                                                       "process)" if dev_list else "")),
+                   "route": ("device-list" if dev_list else
+                             "torch.distributed" if world > 1 else "single-device")},
         "rhat_max_median_file": round(float(np.median(rh_file)), 4),
         "rhat_max_worst_file": round(float(np.max(rh_file)), 4),
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TF,
@@ -550,11 +650,49 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it):
         r["traffic_source"] = traffic["source"]
     for b in batches:
         b.close()
+    bufs.clear()
+    if n_units == 1:
+        # Config 5 scales strongly (256 files in total), and each GPU's share is an
+        # independent launch: N GPUs take as long as 256/N files on one GPU (plus the
+        # gather), which this GPU measures -- the floor being one file's slowest chain.
+        line["strong_scaling_est"] = strong_scaling_est(
+            lambda n: batch_for(0, file_problems(0, conf["files"] // n), 0),
+            conf["files"], C * S_it, line["ms_per_step"])
+    if world > 1 and not args.no_device_list:
+        hb = dist.new_group(backend="gloo")   # host barrier: no collective kernel on the GPUs
+        dist.barrier(group=hb)
+        if rank == 0:
+            every = file_problems(0, conf["files"])
+            line["device_list"] = device_list_leg(
+                lambda step, devs: batch_for(step, every, 0, devs), _dl_devices(world),
+                conf["files"] // world * C * S_it, dev, f_grad(conf["N"], NN), is_batch=True)
+        dist.barrier(group=hb)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def strong_scaling_est(make, files, draws_per_file, ms_1):
+    """Per-GPU share of a strong-scaling run of `files` files on n GPUs, timed on this
+    one GPU: a batch of files/n files (one untimed run, then one timed).  The
+    estimate ignores the gather (a few MB per GPU over xGMI) and assumes the GPUs do
+    not slow one another (independent launches, no collective during sampling)."""
+    import torch
+    out = []
+    for n in (2, 4, 8):
+        with make(n) as b:
+            b.run()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            b.run()
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3
+        out.append({"n_gpus": n, "files_per_gpu": files // n, "ms_per_step_est": round(ms, 2),
+                    "value_est": round(files * draws_per_file / (ms / 1e3), 2),
+                    "efficiency_est": round(ms_1 / (n * ms), 4)})
+    return out
 
 
 if __name__ == "__main__":

@@ -481,6 +481,8 @@ def fitExpGP(x, y, uy, dataType=2, Nn=10, gridType="internal", method="sample",
                 fit.par[k] = g[k][0]
         return {"fit": fit, "method": method, "xGP": xGP, "prior_PD": prior_PD,
                 "lasso": prior_type == "lasso"}
+    if n_gpus is not None and not 1 <= int(n_gpus) <= 16:
+        raise ValueError("fitExpGP: n_gpus must be in 1..16")   # as the R shim (fitoct_devices)
     if devices is None:
         devices = tuple(range(int(device), int(device) + int(n_gpus))) if n_gpus and n_gpus > 1 else ()
     cfg = SamplerConfig(chains=nb_chains, warmup=nb_warmup, samples=nb_sample, seed=seed,

@@ -54,6 +54,21 @@ using namespace fitoct;
   } while (0)
 
 
+int fitoct::check_init(int C, int D, const double* q, const double* eps, const double* minv) {
+  if (eps)
+    for (int c = 0; c < C; ++c)
+      if (!(eps[c] > 0.0 && eps[c] < INFINITY))
+        return fail(FITOCT_E_ARG, "stepsize must be finite and > 0");
+  if (minv)
+    for (size_t i = 0; i < (size_t)C * D; ++i)
+      if (!(minv[i] > 0.0 && minv[i] < INFINITY))
+        return fail(FITOCT_E_ARG, "inv_metric must be finite and > 0");
+  if (q)
+    for (size_t i = 0; i < (size_t)C * D; ++i)
+      if (!isfinite(q[i])) return fail(FITOCT_E_ARG, "q_init must be finite");
+  return FITOCT_OK;
+}
+
 struct fitoct_evaluator {
   fitoct_plan* pl = nullptr;
   int capacity = 0, D = 0, cur_n = -1;
@@ -806,17 +821,8 @@ int32_t fitoct_plan_set_init(fitoct_plan* pl, const double* q_init, const double
     if (pl->launched) return fail(FITOCT_E_ARG, "plan is running: call fitoct_plan_wait first");
     const int C = pl->kp.chains, D = pl->kp.D;
     // checked on the host: the kernel takes every value as given
-    if (stepsize)
-      for (int c = 0; c < C; ++c)
-        if (!(stepsize[c] > 0.0 && stepsize[c] < INFINITY))
-          return fail(FITOCT_E_ARG, "stepsize must be finite and > 0");
-    if (inv_metric)
-      for (size_t i = 0; i < (size_t)C * D; ++i)
-        if (!(inv_metric[i] > 0.0 && inv_metric[i] < INFINITY))
-          return fail(FITOCT_E_ARG, "inv_metric must be finite and > 0");
-    if (q_init)
-      for (size_t i = 0; i < (size_t)C * D; ++i)
-        if (!isfinite(q_init[i])) return fail(FITOCT_E_ARG, "q_init must be finite");
+    const int ck = check_init(C, D, q_init, stepsize, inv_metric);
+    if (ck) return ck;
     HIP_TRY(hipSetDevice(pl->cfg.device));
     if ((q_init || stepsize || inv_metric) && !pl->d_init)
       HIP_TRY(hipMalloc(&pl->d_init, sizeof(double) * (size_t)C * (1 + 2 * D)));
@@ -1126,6 +1132,7 @@ int32_t fitoct_rank_rhat(const double* x, int32_t chains, int32_t n, double* rha
 namespace {
 void free_batch(fitoct_batch* b) {
   if (!b) return;
+  if (b->h_cancel) (void)hipHostFree(b->h_cancel);
   for (fitoct_batch* sb : b->subs) free_batch(sb);
   for (fitoct_plan* pl : b->plans) free_plan(pl);
   (void)hipFree(b->d_kp);
@@ -1217,6 +1224,11 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
       HIP_TRY(hipMalloc(&b->d_map, sizeof(int) * map.size()));
       HIP_TRY(hipMemcpy(b->d_map, map.data(), sizeof(int) * map.size(), hipMemcpyHostToDevice));
       HIP_TRY(hipMalloc(&b->d_kp, sizeof(KParams) * n_problems));
+      // cancellation flag (set by the multi-device layer when another device fails)
+      HIP_TRY(hipHostMalloc((void**)&b->h_cancel, sizeof(int),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+      *b->h_cancel = 0;
+      HIP_TRY(hipHostGetDevicePointer((void**)&b->d_cancel, b->h_cancel, 0));
       HIP_TRY(hipEventCreate(&b->ev0));
       HIP_TRY(hipEventCreate(&b->ev1));
       return FITOCT_OK;
@@ -1241,10 +1253,9 @@ int32_t fitoct_batch_get_info(const fitoct_batch* b, fitoct_plan_info* info) {
   });
 }
 
-int32_t fitoct_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
-  return guarded(__func__, [&]() -> int32_t {
-    if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
-    if (!b->subs.empty()) return group_batch_run(b, d_draws, stream);
+}  // extern "C"
+
+int fitoct::batch_run_single(fitoct_batch* b, void* d_draws, void* stream) {
     HIP_TRY(hipSetDevice(b->cfg.device));
     const size_t P = b->plans.size();
     double* dst = (double*)d_draws;
@@ -1258,6 +1269,7 @@ int32_t fitoct_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
       fitoct_plan* pl = b->plans[p];
       kp[p] = pl->kp;
       kp[p].draws = (double*)((char*)dst + b->per_bytes * p);
+      kp[p].cancel = b->d_cancel;
       pl->last_draws = kp[p].draws;
       HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * pl->kp.chains, st));
     }
@@ -1276,6 +1288,16 @@ int32_t fitoct_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
     }
     b->ran = true;
     return FITOCT_OK;
+}
+
+extern "C" {
+
+int32_t fitoct_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
+  return guarded(__func__, [&]() -> int32_t {
+    if (!b) return fail(FITOCT_E_ARG, "batch is NULL");
+    if (!b->subs.empty()) return group_batch_run(b, d_draws, stream);
+    if (b->h_cancel) __atomic_store_n(b->h_cancel, 0, __ATOMIC_SEQ_CST);
+    return batch_run_single(b, d_draws, stream);
   });
 }
 

@@ -18,8 +18,11 @@
 
 #include <algorithm>
 #include <memory>
+#include <mutex>
+#include <set>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "fitoct.h"
@@ -132,6 +135,57 @@ int own_stream(int dev, hipStream_t& st) {
   return FITOCT_OK;
 }
 
+// Peer access between the gather buffer's device and a shard's device, enabled once per
+// pair and direction for the process (hipMemcpyPeer then moves the block over xGMI; without
+// it the runtime stages the copy through host memory).  A pair the hardware cannot map is
+// remembered too and left to the staged copy.
+int enable_peer(int gdev, int sdev) {
+  if (gdev < 0 || gdev == sdev) return FITOCT_OK;
+  static std::mutex mu;
+  static std::set<std::pair<int, int>> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count({gdev, sdev})) return FITOCT_OK;
+  int can_g = 0, can_s = 0;
+  HIP_TRY(hipDeviceCanAccessPeer(&can_g, gdev, sdev));
+  HIP_TRY(hipDeviceCanAccessPeer(&can_s, sdev, gdev));
+  const std::pair<int, int> dirs[2] = {{gdev, sdev}, {sdev, gdev}};
+  const int can[2] = {can_g, can_s};
+  for (int i = 0; i < 2; ++i) {
+    if (!can[i]) continue;
+    HIP_TRY(hipSetDevice(dirs[i].first));
+    const hipError_t e = hipDeviceEnablePeerAccess(dirs[i].second, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();   // enabled elsewhere
+    else HIP_TRY(e);
+  }
+  done.insert({gdev, sdev});
+  return FITOCT_OK;
+}
+
+// The ordering rule of fitoct_plan_run for a caller buffer (include/fitoct.h): an event
+// recorded on the buffer device's NULL stream, which every in-place shard's private stream
+// waits on before its first write into the buffer.
+struct NullStreamFence {
+  hipEvent_t ev = nullptr;
+  int dev = -1;
+  ~NullStreamFence() {
+    if (ev) {
+      (void)hipSetDevice(dev);
+      (void)hipEventDestroy(ev);
+    }
+  }
+  int record(int gdev) {
+    dev = gdev;
+    HIP_TRY(hipSetDevice(gdev));
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ev, nullptr));
+    return FITOCT_OK;
+  }
+  int order(hipStream_t st) const {
+    if (ev) HIP_TRY(hipStreamWaitEvent(st, ev, 0));
+    return FITOCT_OK;
+  }
+};
+
 size_t chain_bytes(const fitoct_plan* sh) {
   return sizeof(double) * (size_t)sh->kp.iters_saved * sh->kp.ncols;
 }
@@ -189,6 +243,10 @@ int group_plan_set_init(fitoct_plan* pl, const double* q, const double* eps, con
   const int D = pl->kp.D;
   for (const fitoct_plan* sh : pl->shards)
     if (sh->launched) return fail(FITOCT_E_ARG, "plan is running: call fitoct_plan_wait first");
+  // every block is checked before any shard takes its part: a rejected value leaves the
+  // whole plan as it was (no half warm-started plan)
+  const int ck = check_init(pl->kp.chains, D, q, eps, minv);
+  if (ck) return ck;
   DeviceRestore keep;
   for (size_t r = 0; r < pl->shards.size(); ++r) {
     const size_t o = (size_t)pl->shard_off[r];
@@ -201,8 +259,8 @@ int group_plan_set_init(fitoct_plan* pl, const double* q, const double* eps, con
 
 int group_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
   if (stream)
-    return fail(FITOCT_E_ARG, "a multi-device plan runs on each device's default stream: "
-                              "pass stream = NULL");
+    return fail(FITOCT_E_ARG, "a multi-device plan runs each device on a private stream of "
+                              "the library: pass stream = NULL");
   for (const fitoct_plan* sh : pl->shards)
     if (sh->launched) return fail(FITOCT_E_ARG, "plan is running: call fitoct_plan_wait first");
   int gdev = -1;
@@ -211,15 +269,29 @@ int group_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
     if (rc) return rc;
   }
   DeviceRestore keep;
+  NullStreamFence fence;
+  if (d_draws) {
+    bool any_direct = false;
+    for (const fitoct_plan* sh : pl->shards) {
+      any_direct = any_direct || in_place(d_draws, sh->cfg.device, gdev);
+      const int e = enable_peer(gdev, sh->cfg.device);
+      if (e) return e;
+    }
+    if (any_direct) {
+      const int e = fence.record(gdev);
+      if (e) return e;
+    }
+  }
   for (size_t r = 0; r < pl->shards.size(); ++r) {
     fitoct_plan* sh = pl->shards[r];
-    // a shard on the buffer's device writes its block in place; the others are copied
-    // over xGMI once they finish (group_plan_wait)
-    void* dst = in_place(d_draws, sh->cfg.device, gdev)
-                    ? (char*)d_draws + chain_bytes(sh) * (size_t)pl->shard_off[r]
-                    : nullptr;
+    // a shard on the buffer's device writes its block in place (after the caller's NULL
+    // stream work, the fence); the others are copied over xGMI once they finish
+    // (group_plan_wait)
+    const bool direct = in_place(d_draws, sh->cfg.device, gdev);
+    void* dst = direct ? (char*)d_draws + chain_bytes(sh) * (size_t)pl->shard_off[r] : nullptr;
     int rc = FITOCT_OK;
     if (!sh->own_stream) rc = own_stream(sh->cfg.device, sh->own_stream);
+    if (!rc && direct) rc = fence.order(sh->own_stream);
     if (!rc) rc = fitoct_plan_launch(sh, dst, sh->own_stream);
     if (rc) {   // stop what was launched before reporting
       const std::string msg = g_last_error;
@@ -392,15 +464,36 @@ int group_batch_info(const fitoct_batch* b, fitoct_plan_info* info) {
 
 int group_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
   if (stream)
-    return fail(FITOCT_E_ARG, "a multi-device batch runs on each device's default stream: "
-                              "pass stream = NULL");
+    return fail(FITOCT_E_ARG, "a multi-device batch runs each device on a private stream of "
+                              "the library: pass stream = NULL");
   int gdev = -1;
   if (d_draws) {
     const int rc = buffer_device(d_draws, gdev);
     if (rc) return rc;
   }
+  const int n = (int)b->subs.size();
   DeviceRestore keep;
-  const int rc = on_devices((int)b->subs.size(), [&](int r) -> int {
+  NullStreamFence fence;
+  if (d_draws) {
+    bool any_direct = false;
+    for (const fitoct_batch* sb : b->subs) {
+      any_direct = any_direct || in_place(d_draws, sb->cfg.device, gdev);
+      const int e = enable_peer(gdev, sb->cfg.device);
+      if (e) return e;
+    }
+    if (any_direct) {
+      const int e = fence.record(gdev);
+      if (e) return e;
+    }
+  }
+  // every flag is cleared before any device starts, so a cancellation raised by an early
+  // failure is never undone by a later device's start
+  for (fitoct_batch* sb : b->subs) __atomic_store_n(sb->h_cancel, 0, __ATOMIC_SEQ_CST);
+  auto cancel_others = [&](int r) {
+    for (int k = 0; k < n; ++k)
+      if (k != r) __atomic_store_n(b->subs[k]->h_cancel, 1, __ATOMIC_SEQ_CST);
+  };
+  const int rc = on_devices(n, [&](int r) -> int {
     fitoct_batch* sb = b->subs[r];
     char* slice = d_draws ? (char*)d_draws + b->per_bytes * (size_t)b->sub_off[r] : nullptr;
     const bool direct = in_place(d_draws, sb->cfg.device, gdev);
@@ -408,8 +501,23 @@ int group_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
       const int e = own_stream(sb->cfg.device, sb->own_stream);
       if (e) return e;
     }
-    const int e = fitoct_batch_run(sb, direct ? slice : nullptr, sb->own_stream);
-    if (e) return e;
+    if (direct) {
+      const int e = fence.order(sb->own_stream);
+      if (e) return e;
+    }
+    // FITOCT_TEST_FAIL_ENTRY=r (tests only): device entry r fails before its launch, so
+    // one GPU can exercise the cancellation of the other entries
+    static const char* inject = getenv("FITOCT_TEST_FAIL_ENTRY");
+    int e = (inject && atoi(inject) == r)
+                ? fail(FITOCT_E_INTERNAL, "injected failure (FITOCT_TEST_FAIL_ENTRY)")
+                : batch_run_single(sb, direct ? slice : nullptr, sb->own_stream);
+    if (e) {   // the call fails: the other devices' chains stop at their next checked boundary
+      cancel_others(r);
+      return e;
+    }
+    // A failed chain of one file (non-finite init, step-size search) is that file's status
+    // at download, as in a one-device batch: files are independent fits (FitOCT.R:70-124)
+    // and the other files, on this device or another, run on.
     if (d_draws && !direct)
       HIP_TRY(hipMemcpyPeer(slice, gdev, sb->d_draws, sb->cfg.device,
                             b->per_bytes * sb->plans.size()));

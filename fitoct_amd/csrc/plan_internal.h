@@ -62,6 +62,10 @@ struct fitoct_batch {
   double kernel_ms = 0.0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool ran = false;
+  // host-pinned flag polled by every problem's chains (KParams::cancel): set by the
+  // multi-device layer when another device's chain failed; cleared by each run
+  int* h_cancel = nullptr;
+  int* d_cancel = nullptr;    // its device alias
 
   // ---- multi-device batch: problems [sub_off[r], sub_off[r] + subs[r]->plans.size())
   // on sub-batch r, one device each (multi_device.cpp) ----
@@ -96,6 +100,10 @@ int group_batch_create(const fitoct_problem* probs, int n_problems, const fitoct
                        const std::vector<int>& devs, fitoct_batch** out);
 int group_batch_info(const fitoct_batch* b, fitoct_plan_info* info);
 int group_batch_run(fitoct_batch* b, void* d_draws, void* stream);
+// a single-device batch's run (fitoct_batch_run without clearing the cancel flag)
+int batch_run_single(fitoct_batch* b, void* d_draws, void* stream);
+// warm-restart inputs of C chains checked on the host (fitoct_plan_set_init's rules)
+int check_init(int C, int D, const double* q, const double* eps, const double* minv);
 int group_batch_download(fitoct_batch* b, int problem, fitoct_result* res);
 
 }  // namespace fitoct

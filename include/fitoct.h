@@ -126,7 +126,8 @@ typedef struct fitoct_result {
   int64_t draws_capacity;   /* elements available at draws */
   double* stepsize;         /* [chains] adapted step size */
   double* inv_metric;       /* [chains][D] adapted diagonal inverse metric */
-  double* last_q;           /* [chains][D] final unconstrained position */
+  double* last_q;           /* [chains][D] final unconstrained position (NaN, as stepsize
+                               and inv_metric, for a chain whose status is FITOCT_E_TIMEOUT) */
   int32_t* chain_status;    /* [chains] 0 or a fitoct_status per chain */
   int32_t n_cols;           /* out */
   int32_t iters_saved;      /* out */
@@ -214,12 +215,18 @@ int32_t fitoct_plan_get_info(const fitoct_plan* plan, fitoct_plan_info* info);
 /* Run the sampler on `stream` (hipStream_t; NULL = default stream).  If d_draws is
  * non-NULL the draws go to that caller-owned DEVICE buffer (>= info.draws_bytes),
  * otherwise to a plan-internal one.  Returns after the kernel completes.
- * Multi-device plans (cfg.n_devices > 1): `stream` must be NULL (each device runs on
- * its default stream); d_draws may live on any device: the shards on that device write
- * their blocks in place and every other block is copied into it peer-to-peer over xGMI
- * once its device has finished (the one gather of SURVEY.md §8e, inside one process).
+ * Multi-device plans (cfg.n_devices > 1): `stream` must be NULL.  Each device's shard
+ * runs on a private non-blocking stream of the library (shards never order against
+ * each other); d_draws may live on any device: the shards on that device write their
+ * blocks in place and every other block is copied into it peer-to-peer over xGMI once
+ * its device has finished (the one gather of SURVEY.md §8e, inside one process; peer
+ * access between the buffer's device and each shard's device is enabled on first use).
+ * Ordering rule: the in-place shards start after all work the caller queued on the
+ * buffer device's NULL stream before this call (an event recorded there), so a fill or
+ * copy into d_draws issued on that stream cannot land after the draws.
  * The poll / cancel / wait / download / set_init calls below act on every device; a
- * failure on one device cancels the others and the call returns that one status. */
+ * failure on one device cancels the others and the call returns that one status.
+ * set_init checks every block before any device takes its part. */
 int32_t fitoct_plan_run(fitoct_plan* plan, void* d_draws, void* stream);
 /* The same run in two halves, for long fits driven from an interactive host.  It
  * replaces the progress that rstan writes to stan.log and the Shiny server reads
@@ -264,7 +271,13 @@ void fitoct_plan_destroy(fitoct_plan* plan);
  * as global chain cfg->chain_offset + p*cfg->chains + c, so problem p's draws
  * equal a single plan of it with chain_offset = cfg->chain_offset + p*chains.
  * Draws land in [n_problems][chains][iters_saved][n_cols] (caller device buffer
- * of info.draws_bytes, or internal).  Caller buffers are not retained. */
+ * of info.draws_bytes, or internal).  Caller buffers are not retained.
+ * With a device list (cfg.n_devices > 1) the files are split into contiguous blocks,
+ * one sub-batch per device (stream must be NULL; the ordering rule of fitoct_plan_run
+ * applies to d_draws).  When one device's run fails (a HIP error: the call returns that
+ * status) the other devices' chains stop at their next checked transition boundary
+ * instead of running on.  A failed chain of one file (e.g. FITOCT_E_INIT) is only that
+ * file's status at download, with or without a device list: files are independent fits. */
 typedef struct fitoct_batch fitoct_batch;
 int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
                             const fitoct_config* cfg, fitoct_batch** out);

@@ -39,17 +39,86 @@ fitoct_problem <- function(x, y, uy, dataType, Nn, gridType, rho_scale, theta0, 
 # parses them from its stan.log sink, server.R:391-393,457-484)
 # devices: GPU ordinals; the library splits the chains over them (one host thread per
 # GPU), which replaces options(mc.cores = parallel::detectCores()) (FitOCT.R:13, server.R:19)
+# Up to `csv_max_chains` chains the fit goes through one CmdStan CSV per chain and
+# rstan::read_stan_csv (the stanfit rstan itself builds); above it (config 4: 8192 chains
+# of 1500 rows) the draws come back from .Call as one binary array and fitoct_stanfit
+# assembles the same stanfit object without any text round trip.
 fitoct_sample <- function(prob, nb_chains, nb_warmup, nb_iter, seed, adapt_delta,
-                          max_treedepth, devices) {
+                          max_treedepth, devices, csv_max_chains = 64L) {
+  ctrl <- list(chains = as.integer(nb_chains), warmup = as.integer(nb_warmup),
+               samples = as.integer(nb_iter - nb_warmup), seed = as.double(seed),
+               adapt_delta = as.double(adapt_delta), max_treedepth = as.integer(max_treedepth),
+               devices = as.integer(devices))
+  if (nb_chains > csv_max_chains)
+    return(fitoct_stanfit(.Call(fitoct_R_sample_bulk, prob, ctrl), ctrl))
   files <- vapply(seq_len(nb_chains), function(i) tempfile(fileext = '.csv'), character(1))
   on.exit(unlink(files))
-  .Call(fitoct_R_sample, prob,
-        list(chains = as.integer(nb_chains), warmup = as.integer(nb_warmup),
-             samples = as.integer(nb_iter - nb_warmup), seed = as.double(seed),
-             adapt_delta = as.double(adapt_delta), max_treedepth = as.integer(max_treedepth),
-             devices = as.integer(devices)),
-        files)
+  .Call(fitoct_R_sample, prob, ctrl, files)
   rstan::read_stan_csv(files)
+}
+
+# A stanfit from fitoct_R_sample_bulk's arrays, assembled as rstan::read_stan_csv assembles
+# it from CmdStan CSV files (the same sim slot: per-chain named draw vectors with the
+# sampler_params / adaptation_info / elapsed_time / args attributes, warmup2, n_save,
+# permutation), so print(), extract(), as.matrix(), summary(), traceplot(inc_warmup = TRUE)
+# and get_sampler_params() read it as they read the CSV route's fit (plotExpGP.R:7-44,
+# server.R:88-237).  res$draws: array [rows, 7 + n_params, chains], warmup rows first.
+fitoct_stanfit <- function(res, ctrl, model_name = 'ExpGP') {
+  d <- res$draws
+  rows <- dim(d)[1]
+  chains <- dim(d)[3]
+  cols <- dimnames(d)[[2]]
+  lead <- cols[1:7]                                   # lp__, then the 6 sampler columns
+  par_cols <- cols[-(1:7)]
+  flat <- sub('\\.([0-9]+)$', '[\\1]', par_cols)      # theta.1 -> theta[1] (Stan's flatnames)
+  base <- sub('\\[[0-9]+\\]$', '', flat)
+  pars_oi <- c(unique(base), 'lp__')
+  dims_oi <- c(lapply(unique(base), function(b) {
+    n <- sum(base == b)
+    if (n == 1 && !grepl('\\[', flat[match(b, base)])) integer(0) else n
+  }), list(integer(0)))
+  names(dims_oi) <- pars_oi
+  fnames_oi <- c(flat, 'lp__')
+  warmup2 <- ctrl$warmup                              # save_warmup: warmup rows are kept
+  n_kept <- rows - warmup2
+  samples <- lapply(seq_len(chains), function(k) {
+    m <- d[, , k]
+    draws <- c(lapply(seq_along(par_cols), function(j) m[, 7 + j]), list(m[, 1]))
+    names(draws) <- fnames_oi
+    sp <- as.data.frame(m[, 2:7, drop = FALSE])
+    names(sp) <- lead[2:7]
+    attr(draws, 'sampler_params') <- sp
+    attr(draws, 'adaptation_info') <- paste0(
+      '# Adaptation terminated\n# Step size = ', format(res$stepsize[k], digits = 8),
+      '\n# Diagonal elements of inverse mass matrix:\n# ',
+      paste(format(res$inv_metric[, k], digits = 8), collapse = ', '), '\n')
+    attr(draws, 'elapsed_time') <- c(warmup = res$elapsed[1, k], sample = res$elapsed[2, k])
+    post <- if (n_kept > 0) (warmup2 + 1):rows else integer(0)
+    attr(draws, 'mean_pars') <- vapply(draws[seq_along(par_cols)],
+                                       function(v) mean(v[post]), numeric(1))
+    attr(draws, 'mean_lp__') <- mean(m[post, 1])
+    attr(draws, 'args') <- list(sampler_t = 'NUTS(diag_e)', chain_id = k, iter = rows,
+                                warmup = warmup2, thin = 1L, seed = ctrl$seed,
+                                method = 'sampling', save_warmup = TRUE,
+                                control = list(adapt_delta = ctrl$adapt_delta,
+                                               max_treedepth = ctrl$max_treedepth))
+    draws
+  })
+  sim <- list(samples = samples, iter = rows, thin = 1L, warmup = warmup2, chains = chains,
+              n_save = rep(rows, chains), warmup2 = rep(warmup2, chains),
+              permutation = lapply(seq_len(chains), function(k) sample.int(n_kept)),
+              pars_oi = pars_oi, dims_oi = dims_oi, fnames_oi = fnames_oi,
+              n_flatnames = length(fnames_oi))
+  stan_args <- lapply(seq_len(chains), function(k) attr(samples[[k]], 'args'))
+  null_dso <- new('cxxdso', sig = list(character(0)), dso_saved = FALSE,
+                  dso_filename = character(0), modulename = character(0),
+                  system = R.version$system, cxxflags = character(0),
+                  .CXXDSOMISC = new.env(parent = emptyenv()))
+  null_sm <- new('stanmodel', model_name = model_name, model_code = character(0),
+                 model_cpp = list(), dso = null_dso)
+  new('stanfit', model_name = model_name, model_pars = pars_oi, par_dims = dims_oi,
+      mode = 0L, sim = sim, inits = list(), stan_args = stan_args, stanmodel = null_sm,
+      date = date(), .MISC = new.env(parent = emptyenv()))
 }
 
 # rstan::optimizing(as_vector = FALSE, hessian = TRUE): par grouped by base name
@@ -83,7 +152,6 @@ fitExpGP <- function(x, y, uy, dataType = 2, Nn = 10, gridType = 'internal',
                      backend = c('hip', 'rstan'), device = 0L, n_gpus = 1L) {
   backend <- match.arg(backend)
   prior_type <- match.arg(prior_type)
-  devices <- fitoct_devices(device, n_gpus)
   if (backend == 'rstan')
     return(FitOCTLib::fitExpGP(x = x, y = y, uy = uy, dataType = dataType, Nn = Nn,
                                gridType = gridType, method = method, theta0 = theta0,
@@ -91,6 +159,7 @@ fitExpGP <- function(x, y, uy, dataType = 2, Nn = 10, gridType = 'internal',
                                rho_scale = rho_scale, nb_warmup = nb_warmup,
                                nb_iter = nb_iter, prior_PD = prior_PD,
                                open_progress = open_progress))
+  devices <- fitoct_devices(device, n_gpus)   # after the rstan return: no HIP call for it
   prob <- fitoct_problem(x, y, uy, dataType, Nn, gridType, rho_scale, theta0, Sigma0,
                          match(prior_type, c('normal', 'lasso', 'horseshoe')) - 1L,
                          lambda_rate, lambda_scale, nu, prior_PD)
@@ -112,9 +181,9 @@ fitMonoExp <- function(x, y, uy, dataType = 2, method = 'optim', nb_warmup = 500
                        seed = sample.int(.Machine$integer.max, 1),
                        backend = c('hip', 'rstan'), device = 0L, n_gpus = 1L) {
   backend <- match.arg(backend)
-  devices <- fitoct_devices(device, n_gpus)
   if (backend == 'rstan')
     return(FitOCTLib::fitMonoExp(x = x, y = y, uy = uy, dataType = dataType))
+  devices <- fitoct_devices(device, n_gpus)
   theta0 <- .Call(fitoct_R_mono_theta0, as.double(x), as.double(y), as.integer(dataType))
   prob <- fitoct_problem(x, y, uy, dataType, 2L, 'extremal', 0, theta0, diag(3), 3L)
   if (method == 'sample') {

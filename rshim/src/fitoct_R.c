@@ -120,6 +120,75 @@ SEXP fitoct_R_sample(SEXP prob, SEXP ctrl, SEXP files) {
   return R_NilValue;
 }
 
+/* .Call(fitoct_R_sample_bulk, prob, ctrl): the same run as fitoct_R_sample for many chains
+ * (R/fitExpGP.R uses it above 64 chains), returned as R vectors instead of one CSV per chain:
+ * list(draws = array(dim = c(rows, 7 + n_params, chains), dimnames = list(NULL, columns,
+ * NULL)), stepsize [chains], inv_metric [D, chains] matrix, elapsed [2, chains] matrix).
+ * fitoct_drive_sample_bulk writes straight into the R vectors (no copy). */
+SEXP fitoct_R_sample_bulk(SEXP prob, SEXP ctrl) {
+  fitoct_problem p;
+  fitoct_config c;
+  to_problem(prob, &p);
+  fitoct_default_config(&c);
+  c.chains = inum(ctrl, "chains");
+  c.warmup = inum(ctrl, "warmup");
+  c.samples = inum(ctrl, "samples");
+  c.seed = (uint64_t)num(ctrl, "seed");
+  c.adapt_delta = num(ctrl, "adapt_delta");
+  c.max_treedepth = inum(ctrl, "max_treedepth");
+  SEXP devs = elt(ctrl, "devices");
+  if (TYPEOF(devs) != INTSXP || XLENGTH(devs) < 1 || XLENGTH(devs) > FITOCT_MAX_DEVICES)
+    Rf_error("fitoct: devices must be an integer vector of 1 to %d device ordinals",
+             FITOCT_MAX_DEVICES);
+  c.device = INTEGER(devs)[0];
+  c.n_devices = (int32_t)XLENGTH(devs);
+  for (int i = 0; i < c.n_devices; ++i) c.devices[i] = INTEGER(devs)[i];
+  const int P = fitoct_output_n_params(&p), D = fitoct_dim(p.prior_type, p.Nn);
+  if (P <= 0 || D <= 0 || c.chains < 1 || c.samples < 1 || c.warmup < 0)
+    Rf_error("fitoct: invalid model or chain / iteration counts");
+  const int n_out = 7 + P;
+  const R_xlen_t rows = c.save_warmup ? (R_xlen_t)c.warmup + c.samples : c.samples;
+  SEXP draws = PROTECT(Rf_allocVector(REALSXP, rows * n_out * (R_xlen_t)c.chains));
+  SEXP eps = PROTECT(Rf_allocVector(REALSXP, c.chains));
+  SEXP minv = PROTECT(Rf_allocMatrix(REALSXP, D, c.chains));
+  SEXP el = PROTECT(Rf_allocMatrix(REALSXP, 2, c.chains));
+  const int32_t rc = fitoct_drive_sample_bulk(&p, &c, REAL(draws), (int64_t)XLENGTH(draws),
+                                              REAL(eps), REAL(minv), REAL(el), 50, r_line,
+                                              r_interrupted, NULL);
+  if (rc != FITOCT_OK) {
+    UNPROTECT(4);
+    stop_on(rc);
+  }
+  SEXP dim = PROTECT(Rf_allocVector(INTSXP, 3));
+  INTEGER(dim)[0] = (int)rows;
+  INTEGER(dim)[1] = n_out;
+  INTEGER(dim)[2] = c.chains;
+  Rf_setAttrib(draws, R_DimSymbol, dim);
+  char buf[64];
+  SEXP cn = PROTECT(Rf_allocVector(STRSXP, n_out));
+  static const char* lead[7] = {"lp__", "accept_stat__", "stepsize__", "treedepth__",
+                                "n_leapfrog__", "divergent__", "energy__"};
+  for (int j = 0; j < 7; ++j) SET_STRING_ELT(cn, j, Rf_mkChar(lead[j]));
+  for (int j = 0; j < P; ++j) {
+    fitoct_output_param_name(&p, j, buf, (int32_t)sizeof buf);
+    SET_STRING_ELT(cn, 7 + j, Rf_mkChar(buf));
+  }
+  SEXP dn = PROTECT(Rf_allocVector(VECSXP, 3));
+  SET_VECTOR_ELT(dn, 1, cn);
+  Rf_setAttrib(draws, R_DimNamesSymbol, dn);
+  const char* names[] = {"draws", "stepsize", "inv_metric", "elapsed"};
+  SEXP out = PROTECT(Rf_allocVector(VECSXP, 4));
+  SEXP on = PROTECT(Rf_allocVector(STRSXP, 4));
+  SET_VECTOR_ELT(out, 0, draws);
+  SET_VECTOR_ELT(out, 1, eps);
+  SET_VECTOR_ELT(out, 2, minv);
+  SET_VECTOR_ELT(out, 3, el);
+  for (int i = 0; i < 4; ++i) SET_STRING_ELT(on, i, Rf_mkChar(names[i]));
+  Rf_setAttrib(out, R_NamesSymbol, on);
+  UNPROTECT(9);
+  return out;
+}
+
 /* .Call(fitoct_R_optimize, prob, ctrl): ctrl = list(device, hessian) ->
  * list(par (named, output layout), value, return_code, hessian (D x D, dimnames),
  *      dL, m, resid) -- rstan::optimizing(as_vector = FALSE) after R/fitExpGP.R regroups par */
@@ -207,6 +276,7 @@ SEXP fitoct_R_device_count(void) { return Rf_ScalarInteger(fitoct_device_count()
 
 static const R_CallMethodDef call_methods[] = {
     {"fitoct_R_sample", (DL_FUNC)&fitoct_R_sample, 3},
+    {"fitoct_R_sample_bulk", (DL_FUNC)&fitoct_R_sample_bulk, 2},
     {"fitoct_R_optimize", (DL_FUNC)&fitoct_R_optimize, 2},
     {"fitoct_R_vb", (DL_FUNC)&fitoct_R_vb, 3},
     {"fitoct_R_mono_theta0", (DL_FUNC)&fitoct_R_mono_theta0, 3},

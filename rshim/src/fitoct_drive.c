@@ -125,6 +125,80 @@ int32_t fitoct_drive_sample_csv(const fitoct_problem* prob, const fitoct_config*
   return rc;
 }
 
+/* ---- method = 'sample', many chains -> binary arrays for R ----------------------- */
+int32_t fitoct_drive_bulk_layout(const fitoct_problem* prob, int32_t chains, int64_t rows,
+                                 const double* raw, double* out) {
+  if (!prob || !raw || !out || chains < 1 || rows < 1) return FITOCT_E_ARG;
+  const int32_t ncols = fitoct_n_cols(prob->prior_type, prob->Nn);
+  const int32_t P = fitoct_output_n_params(prob);
+  if (ncols <= 0 || P <= 0) return FITOCT_E_ARG;
+  const int32_t n_out = 7 + P;
+  /* one chain's rows in the output layout, then transposed to column runs */
+  const int64_t blk = rows < 256 ? rows : 256;
+  double* tmp = (double*)malloc(sizeof(double) * (size_t)blk * (size_t)n_out);
+  if (!tmp) return FITOCT_E_INTERNAL;
+  int32_t rc = FITOCT_OK;
+  for (int32_t ch = 0; rc == FITOCT_OK && ch < chains; ++ch) {
+    const double* src = raw + (size_t)ch * (size_t)rows * (size_t)ncols;
+    double* dst = out + (size_t)ch * (size_t)n_out * (size_t)rows;
+    for (int64_t r0 = 0; rc == FITOCT_OK && r0 < rows; r0 += blk) {
+      const int64_t nr = rows - r0 < blk ? rows - r0 : blk;
+      rc = fitoct_output_rows(prob, 7, nr, src + (size_t)r0 * (size_t)ncols, tmp);
+      for (int64_t i = 0; rc == FITOCT_OK && i < nr; ++i)
+        for (int32_t j = 0; j < n_out; ++j)
+          dst[(size_t)j * (size_t)rows + (size_t)(r0 + i)] = tmp[(size_t)i * (size_t)n_out + j];
+    }
+  }
+  free(tmp);
+  return rc;
+}
+
+int32_t fitoct_drive_sample_bulk(const fitoct_problem* prob, const fitoct_config* cfg,
+                                 double* draws, int64_t draws_capacity, double* stepsize,
+                                 double* inv_metric, double* elapsed, int32_t poll_ms,
+                                 fitoct_line_fn line, fitoct_interrupt_fn interrupted, void* ctx) {
+  if (!prob || !cfg || !draws) return FITOCT_E_ARG;
+  const int32_t ncols = fitoct_n_cols(prob->prior_type, prob->Nn);
+  const int32_t P = fitoct_output_n_params(prob);
+  if (cfg->chains < 1 || cfg->warmup < 0 || cfg->samples < 1 || ncols <= 0 || P <= 0) {
+    fitoct_plan* plan = NULL;   /* the library's own argument check sets the message */
+    const int32_t rc = fitoct_plan_create(prob, cfg, &plan);
+    fitoct_plan_destroy(plan);
+    return rc != FITOCT_OK ? rc : FITOCT_E_ARG;
+  }
+  const int64_t rows = cfg->save_warmup ? (int64_t)cfg->warmup + cfg->samples : cfg->samples;
+  if (draws_capacity < (int64_t)cfg->chains * (7 + P) * rows) return FITOCT_E_ARG;
+  const size_t n_raw = (size_t)cfg->chains * (size_t)rows * (size_t)ncols;
+  double* raw = (double*)malloc(sizeof(double) * n_raw);
+  if (!raw) return FITOCT_E_INTERNAL;
+  fitoct_result r;
+  memset(&r, 0, sizeof r);
+  r.draws = raw;
+  r.draws_capacity = (int64_t)n_raw;
+  r.stepsize = stepsize;
+  r.inv_metric = inv_metric;
+  csv_ctx c = {line, interrupted, ctx, cfg->warmup, cfg->samples, -1};
+  int32_t rc = fitoct_drive_sample(prob, cfg, &r, poll_ms, csv_progress, csv_interrupted, &c);
+  if (rc == FITOCT_OK && elapsed) {
+    const int64_t wrows = cfg->save_warmup ? cfg->warmup : 0;
+    const double t = r.kernel_ms / 1e3;
+    for (int32_t ch = 0; ch < cfg->chains; ++ch) {
+      const double* d = raw + (size_t)ch * (size_t)rows * (size_t)ncols;
+      double lw = 0.0, ls = 0.0;       /* n_leapfrog__ (column 4) per phase */
+      for (int64_t i = 0; i < rows; ++i) {
+        const double v = d[(size_t)i * ncols + 4];
+        if (i < wrows) lw += v;
+        else ls += v;
+      }
+      elapsed[2 * ch] = (lw + ls > 0.0) ? t * lw / (lw + ls) : 0.0;
+      elapsed[2 * ch + 1] = t - elapsed[2 * ch];
+    }
+  }
+  if (rc == FITOCT_OK) rc = fitoct_drive_bulk_layout(prob, cfg->chains, rows, raw, draws);
+  free(raw);
+  return rc;
+}
+
 /* ---- method = 'optim' ---------------------------------------------------------- */
 /* theta and yGP of an output-layout row (yGP found by name: a parameter of the normal
  * and lasso families, a transformed parameter of the horseshoe) */

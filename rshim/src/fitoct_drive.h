@@ -45,6 +45,29 @@ int32_t fitoct_drive_sample_csv(const fitoct_problem* prob, const fitoct_config*
                                 const char* const* paths, int32_t poll_ms, fitoct_line_fn line,
                                 fitoct_interrupt_fn interrupted, void* ctx);
 
+/* fitExpGP(method = 'sample') for many chains (config 4: 8192), where one Stan CSV file per
+ * chain (fitoct_drive_sample_csv: ~1500 text rows each, parsed by rstan::read_stan_csv)
+ * does not scale.  Same run, progress and interrupts as fitoct_drive_sample_csv; the
+ * outputs stay binary and land in caller buffers that R allocates as its own vectors:
+ *  - draws [chains][n_out][rows], n_out = 7 + fitoct_output_n_params(prob): per chain,
+ *    every output column (the 7 sampler columns lp__ .. energy__, then the parameters,
+ *    transformed parameters and br of the output layout) as one contiguous run of
+ *    `rows` = iters_saved values.  This is R's column-major array(dim = c(rows, n_out,
+ *    chains)): the wrapper hands it, unchanged, to the stanfit constructor
+ *    (rshim/R/fitExpGP.R:fitoct_stanfit);
+ *  - stepsize [chains], inv_metric [chains][D] (Stan's adaptation info);
+ *  - elapsed [chains][2]: warmup / sampling seconds (the kernel time split by each
+ *    chain's n_leapfrog__ in each phase, as in the CSV trailer).
+ * draws_capacity is the number of doubles at `draws`.  Host buffers are caller-owned. */
+int32_t fitoct_drive_sample_bulk(const fitoct_problem* prob, const fitoct_config* cfg,
+                                 double* draws, int64_t draws_capacity, double* stepsize,
+                                 double* inv_metric, double* elapsed, int32_t poll_ms,
+                                 fitoct_line_fn line, fitoct_interrupt_fn interrupted, void* ctx);
+/* The layout step alone (host only): raw kernel draws [chains][rows][fitoct_n_cols] ->
+ * out [chains][n_out][rows] as above. */
+int32_t fitoct_drive_bulk_layout(const fitoct_problem* prob, int32_t chains, int64_t rows,
+                                 const double* raw, double* out);
+
 /* method = 'optim' (rstan::optimizing(hessian = TRUE) inside FitOCTLib::fitExpGP /
  * fitMonoExp; read as fit$par$theta, fit$par$br, fit$par$m, fit$par$resid, fit$hessian at
  * plotExpGP.R:13-18, plotMonoExp.R:15-16, server.R:107-172).

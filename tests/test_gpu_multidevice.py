@@ -232,3 +232,74 @@ def test_fitexpgp_n_gpus():
     with pytest.raises(_lib.FitOCTError) as ei:
         fitExpGP(p.x, p.y, p.uy, n_gpus=n + 1, **kw)
     assert ei.value.code == -1 and f"device {n}" in str(ei.value)
+
+
+def test_in_place_shards_wait_for_callers_null_stream_work():
+    """Ordering rule (include/fitoct.h, fitoct_plan_run): the in-place shards run on
+    private non-blocking streams, yet start only after the work the caller queued on the
+    buffer device's NULL stream.  Slow FP64 matmuls and then a NaN fill of the buffer are
+    queued on torch's default (NULL) stream right before run(): without the library's
+    fence the fill would land on top of the draws."""
+    import torch
+    prob = _prob("normal", 600, 10)
+    cfg = SamplerConfig(chains=16, warmup=40, samples=40, seed=19)
+    ref = sample(prob, cfg)
+    assert torch.cuda.current_stream().cuda_stream == 0   # torch's default = NULL stream
+    with Plan(prob, dataclasses.replace(cfg, devices=(0, 0))) as pl:
+        buf = torch.zeros(pl.info["draws_bytes"] // 8, dtype=torch.float64, device="cuda")
+        x = torch.randn(4096, 4096, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+        for _ in range(8):   # ~0.1 s of NULL-stream work ahead of the fill
+            x = (x @ x) * 1e-4
+        buf.fill_(float("nan"))
+        pl.run(d_draws=buf.data_ptr())
+        got = buf.view(ref.draws.shape).cpu().numpy()
+    np.testing.assert_array_equal(got, ref.draws)
+
+
+def test_batch_device_failure_cancels_the_others():
+    """A multi-device batch whose entry 0 fails (FITOCT_TEST_FAIL_ENTRY=0, read once per
+    process, so in a child) returns that status, and the other entries' chains (100k
+    iterations each) are cancelled at a transition boundary instead of running on."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, 'tests'); import test_gpu_multidevice as t; "
+            "t._batch_fail_case()")
+    env = dict(__import__("os").environ, FITOCT_TEST_FAIL_ENTRY="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def _batch_fail_case():
+    import time
+    t0, S0 = default_prior()
+    probs = []
+    for f in range(4):
+        d = synth_decay(481, MODULATIONS[f % 4], 1234 + f)
+        probs.append(ExpGPProblem(d["x"], d["y"], d["uy"], Nn=15, gridType="extremal",
+                                  theta0=t0, Sigma0=S0, prior_type="normal"))
+    cfg = SamplerConfig(chains=4, warmup=50, samples=100000, seed=7, devices=(0, 0))
+    start = time.time()
+    with Batch(probs, cfg) as b:
+        with pytest.raises(_lib.FitOCTError) as ei:
+            b.run()
+    assert ei.value.code == -7 and "injected" in str(ei.value), str(ei.value)
+    assert time.time() - start < 60
+
+
+def test_set_init_checks_every_block_before_any_device():
+    """A warm-restart block rejected on device entry 1 (NaN start) leaves entry 0's
+    block unset too: the plan then runs from the default start, as one device would."""
+    prob = _prob()
+    cfg = SamplerConfig(chains=8, warmup=20, samples=20, seed=4, max_treedepth=6)
+    ref = sample(prob, cfg)
+    with Plan(prob, dataclasses.replace(cfg, devices=(0, 0))) as pl:
+        q = np.zeros((8, prob.D))
+        q[6, 0] = np.nan                   # chain 6: entry 1's block (chains 4..7)
+        with pytest.raises(_lib.FitOCTError) as ei:
+            pl.set_init(q_init=q, stepsize=np.full(8, 0.1))
+        assert ei.value.code == -1 and "q_init" in str(ei.value)
+        pl.run()
+        out = pl.download()
+    _same(out, ref)

@@ -43,6 +43,13 @@ def _drive_lib():
     L.fitoct_drive_sample_csv.argtypes = [C.POINTER(_lib.Problem), C.POINTER(_lib.Config),
                                           C.POINTER(C.c_char_p), C.c_int32, LINE, INTERRUPT,
                                           C.c_void_p]
+    L.fitoct_drive_sample_bulk.restype = C.c_int32
+    L.fitoct_drive_sample_bulk.argtypes = [C.POINTER(_lib.Problem), C.POINTER(_lib.Config),
+                                           _dp, C.c_int64, _dp, _dp, _dp, C.c_int32, LINE,
+                                           INTERRUPT, C.c_void_p]
+    L.fitoct_drive_bulk_layout.restype = C.c_int32
+    L.fitoct_drive_bulk_layout.argtypes = [C.POINTER(_lib.Problem), C.c_int32, C.c_int64, _dp,
+                                           _dp]
     L.fitoct_drive_optimize.restype = C.c_int32
     L.fitoct_drive_optimize.argtypes = [C.POINTER(_lib.Problem), C.POINTER(_lib.OptimConfig),
                                         _dp, _dp, _dp, _dp, _dp, _dp, _dp,
@@ -100,8 +107,52 @@ def _prob(N=512, Nn=10):
 def test_driver_builds_and_exports():
     L = _drive_lib()
     for f in ("fitoct_drive_sample", "fitoct_drive_sample_csv", "fitoct_drive_optimize",
-              "fitoct_drive_vb_csv"):
+              "fitoct_drive_vb_csv", "fitoct_drive_sample_bulk", "fitoct_drive_bulk_layout"):
         assert hasattr(L, f)
+
+
+def _bulk_expected(prob, raw):
+    """fitoct_R_sample_bulk's array from raw kernel draws [chains, rows, n_cols]: every
+    chain's output-layout rows (stanfit.materialise, the CSV writer's layout) transposed to
+    column runs, i.e. R's array(dim = c(rows, n_out, chains)) in memory order."""
+    from fitoct_amd.stanfit import materialise
+    return np.ascontiguousarray(np.transpose(materialise(raw, prob), (0, 2, 1)))
+
+
+@pytest.mark.parametrize("family", ["normal", "lasso", "horseshoe"])
+def test_bulk_layout_matches_output_rows(family):
+    """The host layout step of the bulk route on synthetic raw rows (300 rows, so the
+    256-row blocking is crossed): equal to the per-row output layout, transposed."""
+    t0, S0 = default_prior()
+    d = synth_decay(64, "sincExp", 5)
+    prob = ExpGPProblem(d["x"], d["y"], d["uy"], Nn=6, gridType="extremal", theta0=t0,
+                        Sigma0=S0, prior_type=family)
+    rng = np.random.default_rng(3)
+    raw = rng.uniform(0.1, 2.0, (3, 300, len(prob.column_names())))
+    want = _bulk_expected(prob, raw)
+    out = np.full(want.shape, np.nan)
+    p = prob.to_c()
+    rc = _drive_lib().fitoct_drive_bulk_layout(C.byref(p), 3, 300, raw.ctypes.data_as(_dp),
+                                               out.ctypes.data_as(_dp))
+    assert rc == 0
+    np.testing.assert_array_equal(out, want)
+
+
+def test_bulk_driver_argument_errors():
+    """chains = 0 -> the library's FITOCT_E_ARG; a too small draws buffer -> FITOCT_E_ARG
+    before anything runs (no line, no interrupt poll)."""
+    L = _drive_lib()
+    prob = _prob(N=64)
+    out = np.zeros(10)
+    for cfg in (SamplerConfig(chains=0, warmup=5, samples=5),
+                SamplerConfig(chains=2, warmup=5, samples=5)):
+        p, c = prob.to_c(), cfg.to_c()
+        lines = []
+        cb_l = LINE(lambda _ctx, line: lines.append(line))
+        cb_i = INTERRUPT(lambda _ctx: 0)
+        rc = L.fitoct_drive_sample_bulk(C.byref(p), C.byref(c), out.ctypes.data_as(_dp),
+                                        out.size, None, None, None, 5, cb_l, cb_i, None)
+        assert rc == -1 and lines == []
 
 
 def test_csv_driver_argument_errors(tmp_path):
@@ -272,3 +323,39 @@ def test_vb_driver_csv(tmp_path):
     fit.write_stan_csv(str(tmp_path / "py"))
     r2 = stancsv_reader.read(str(tmp_path / "py" / "chain_vb.csv"))
     np.testing.assert_array_equal(r2["rows"], r["rows"])      # one writer, same file
+
+
+@pytest.mark.gpu
+def test_bulk_driver_at_config4_chain_count():
+    """fitExpGP(nb_chains = 8192) through the bulk route (fitoct_R_sample_bulk ->
+    fitoct_drive_sample_bulk): config 4's shape (lasso, N = 4096, Nn = 15, 8192 chains;
+    short warmup / sampling), the array equals the plan's draws in the output layout
+    transposed to R's [rows, n_out, chains] order, step sizes and metrics equal the
+    plan's, the elapsed split sums to the kernel time and the progress ends at 100 %."""
+    t0, S0 = default_prior()
+    d = synth_decay(4096, "sincExp", 1234)
+    prob = ExpGPProblem(d["x"], d["y"], d["uy"], Nn=15, gridType="extremal", theta0=t0,
+                        Sigma0=S0, prior_type="lasso", lambda_scale=10.0)
+    cfg = SamplerConfig(chains=8192, warmup=15, samples=10, seed=1000, max_treedepth=6)
+    with Plan(prob, cfg) as pl:
+        pl.run()
+        ref = pl.download()
+    want = _bulk_expected(prob, ref.draws)
+    n_out = want.shape[1]
+    out = np.full(want.shape, np.nan)
+    eps, minv = np.empty(8192), np.empty((8192, prob.D))
+    el = np.empty((8192, 2))
+    p, c = prob.to_c(), cfg.to_c()
+    lines = []
+    cb_l = LINE(lambda _ctx, line: lines.append(line.decode()))
+    cb_i = INTERRUPT(lambda _ctx: 0)
+    rc = _drive_lib().fitoct_drive_sample_bulk(
+        C.byref(p), C.byref(c), out.ctypes.data_as(_dp), out.size, eps.ctypes.data_as(_dp),
+        minv.ctypes.data_as(_dp), el.ctypes.data_as(_dp), 20, cb_l, cb_i, None)
+    assert rc == 0, _lib.lib().fitoct_last_error()
+    assert out.shape == (8192, n_out, 25)
+    np.testing.assert_array_equal(out, want)
+    np.testing.assert_array_equal(eps, ref.stepsize)
+    np.testing.assert_array_equal(minv, ref.inv_metric)
+    assert np.all(el >= 0) and np.allclose(el.sum(1), el.sum(1)[0])
+    assert lines and "100%" in lines[-1]
