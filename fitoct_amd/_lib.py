@@ -38,6 +38,7 @@ class Problem(C.Structure):
         ("prior_type", C.c_int32), ("lambda_rate", C.c_double), ("lambda_scale", C.c_double),
         ("nu", C.c_double), ("prior_PD", C.c_int32), ("kernel_conv", C.c_int32),
         ("lambda_conv", C.c_int32), ("sigma_scale", C.c_double), ("nugget", C.c_double),
+        ("theta_prior", C.c_int32),
     ]
 
 
@@ -201,7 +202,7 @@ def _single_hip_runtime():
         pass
 
 
-ABI_VERSION = 4   # include/fitoct.h FITOCT_ABI_VERSION
+ABI_VERSION = 5   # include/fitoct.h FITOCT_ABI_VERSION
 
 
 def lib():

@@ -44,6 +44,9 @@ class ExpGPProblem:
     sigma_scale: float = 10.0
     nugget: float = 1e-9
     B: np.ndarray = None
+    # monoexp only: 1 = theta_k ~ exponential(1/lambda_scale), Tests/testGamma.R's model
+    # (the sampler's known answer, include/fitoct.h theta_prior)
+    theta_prior: int = 0
 
     def __post_init__(self):
         self.x = np.ascontiguousarray(self.x, dtype=np.float64)
@@ -94,6 +97,7 @@ class ExpGPProblem:
         p.lambda_conv = int(self.lambda_conv)
         p.sigma_scale = float(self.sigma_scale)
         p.nugget = float(self.nugget)
+        p.theta_prior = int(self.theta_prior)
         return p
 
     def basis(self):

@@ -90,7 +90,14 @@ int check_problem(const fitoct_problem* p) {
   if (!p->x || !p->y || !p->uy) return fail(FITOCT_E_ARG, "x, y, uy must be non-NULL");
   const bool mono = p->prior_type == FITOCT_MODEL_MONOEXP;
   if (!mono && (p->Nn < 2 || p->Nn > 24)) return fail(FITOCT_E_ARG, "Nn must be in [2, 24]");
-  if (mono && p->prior_PD) return fail(FITOCT_E_ARG, "the mono-exponential model has a flat prior: prior_PD must be 0");
+  if (p->theta_prior != 0 && p->theta_prior != 1)
+    return fail(FITOCT_E_ARG, "theta_prior must be 0 or 1");
+  if (p->theta_prior == 1 && !mono)
+    return fail(FITOCT_E_ARG, "theta_prior = 1 is the mono-exponential model's switch");
+  if (p->theta_prior == 1 && !(p->lambda_scale > 0.0))
+    return fail(FITOCT_E_ARG, "lambda_scale must be > 0");
+  if (mono && p->prior_PD && p->theta_prior == 0)
+    return fail(FITOCT_E_ARG, "the mono-exponential model has a flat prior: prior_PD must be 0");
   if (model_dim(p->prior_type, p->Nn) < 0) return fail(FITOCT_E_ARG, "unknown prior_type");
   if (p->data_type != 1 && p->data_type != 2) return fail(FITOCT_E_ARG, "data_type must be 1 or 2");
   for (int i = 0; i < p->N; ++i) {
@@ -404,6 +411,7 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   k.nu = p->nu;
   k.sigma_scale = p->sigma_scale;
   k.sigma_scale_inv = 1.0 / p->sigma_scale;
+  k.theta_rate = p->theta_prior == 1 ? 1.0 / p->lambda_scale : 0.0;
   k.chains = chains;
 
   // chains per tile: fill every CU with one tile first, then stack chains

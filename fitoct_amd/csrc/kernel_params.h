@@ -67,6 +67,7 @@ struct KParams {
   double nu;                // horseshoe nu
   double sigma_scale;
   double sigma_scale_inv;   // 1 / sigma_scale
+  double theta_rate;        // mono-exp, theta_prior = 1: theta_k ~ exponential(theta_rate)
   // ---- sampler ----
   int chains;               // chains in this launch
   int chain_offset;         // global id of chain 0

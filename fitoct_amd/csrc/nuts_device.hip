@@ -1124,10 +1124,13 @@ struct Chain {
     const double Sd2t = Si[6] * d0 + Si[7] * d1 + Si[8] * d2;
     const double iss = Pr().sigma_scale_inv;   // 1 / sigma_scale (host division)
     const double gyf = lik ? th1 * th2 * is2 : 0.0;   // dlp/dyGP_k = gyf * S[4+k]
+    // mono-exp with theta_prior = 1: theta_k ~ exponential(tr) (Tests/testGamma.R's model)
+    const double tr = mono ? Pr().theta_rate : 0.0;
     double lpc = 0.0;
     if (lane == 0) {
       if (lik) lpc += -(double)Pr().N * usig;
       lpc += -0.5 * (d0 * Sd0 + d1 * Sd1 + d2 * Sd2t) + qs[0] + qs[1] + qs[2];
+      if (mono) lpc += -tr * (th0 + th1 + th2);
       if (!mono) lpc += -0.5 * (sig * iss) * (sig * iss) + usig;
     }
     double ysum = 0.0;   // normal family: sum yGP^2
@@ -1144,6 +1147,7 @@ struct Chain {
           const double thk = (k == 0) ? th0 : (k == 1) ? th1 : th2;
           const double sdk = (k == 0) ? Sd0 : (k == 1) ? Sd1 : Sd2t;
           gk = 1.0 - thk * sdk;
+          if (mono) gk -= tr * thk;
           if (lik) ck = (k == 2) ? th1 * is2 : thk * is2;
         } else if (mono) {
           // no other parameter

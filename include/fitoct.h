@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FITOCT_ABI_VERSION 4
+#define FITOCT_ABI_VERSION 5
 /* largest accepted N (depth bins): bounds every host and device allocation derived from it */
 #define FITOCT_MAX_BINS (1 << 22)
 /* largest device list of one call (fitoct_config.devices) */
@@ -87,6 +87,13 @@ typedef struct fitoct_problem {
   int32_t lambda_conv;   /* ⚑ 0: rate = 1/lambda_rate, 1: rate = lambda_rate */
   double sigma_scale;    /* ⚑ sigma ~ half-normal(0, sigma_scale) */
   double nugget;         /* diagonal jitter of K(xGP,xGP) (1e-9) */
+  /* theta prior of the mono-exponential model (ABI 5).  0: the model's own (flat on
+   * theta > 0).  1: theta_k ~ exponential(1 / lambda_scale) i.i.d. -- Tests/testGamma.R's
+   * model `lambda ~ exponential(1./lambda_scale)` (lambda_scale = 10) on each of the three
+   * coordinates, a proper prior, so prior_PD = 1 samples it alone: the reference's own
+   * known answer for the sampler (mean = sd = lambda_scale; tests/test_gpu_kat.py).
+   * Only with prior_type = FITOCT_MODEL_MONOEXP. */
+  int32_t theta_prior;
 } fitoct_problem;
 
 /* rstan::sampling controls (testGamma.R:42-47) + sharding / device selection. */

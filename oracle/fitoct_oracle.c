@@ -105,6 +105,7 @@ typedef struct {
   double* B;            /* [N][Nn] */
   double th0[3], Si[9]; /* Sigma0^-1 */
   double rate, ls, nu, ss;
+  double trate; /* mono-exp, theta_prior = 1: theta_k ~ exponential(trate) (testGamma.R) */
 } model;
 
 static int dimof(int fam, int Nn) {
@@ -187,9 +188,10 @@ static int model_init(model* m, const fitoct_problem* p) {
     return -1;
   }
   memcpy(m->th0, p->theta0, sizeof m->th0);
-  if (m->fam == 3) { /* flat prior on theta, sigma fixed at 1 */
+  if (m->fam == 3) { /* flat prior on theta (or testGamma.R's exponential), sigma fixed at 1 */
     memset(m->Si, 0, sizeof m->Si);
     m->ss = 1.0;
+    m->trate = p->theta_prior == 1 ? 1.0 / p->lambda_scale : 0.0;
     return 0;
   }
   const double* S = p->Sigma0;
@@ -279,6 +281,11 @@ static double logp_grad(const model* m, const double* q, double* g, double* sumr
     g[j] = th[j] * (gth[j] - sd) + 1.0;
   }
   if (mono) {
+    /* theta_prior = 1 (Tests/testGamma.R:19-28): theta_k ~ exponential(trate) */
+    for (int j = 0; j < 3; ++j) {
+      lp += -m->trate * th[j];
+      g[j] -= m->trate * th[j];
+    }
     if (!isfinite(lp)) lp = -INFINITY;
     return lp;
   }

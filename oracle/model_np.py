@@ -112,6 +112,7 @@ class Problem:
     nugget: float = 1e-9
     B: np.ndarray = None
     xGP: np.ndarray = None
+    theta_prior: int = 0          # monoexp: 1 = theta_k ~ exponential(1/lambda_scale) (testGamma.R)
 
     def __post_init__(self):
         self.x = np.asarray(self.x, np.float64)
@@ -254,6 +255,10 @@ def logp_grad(q, prob: Problem):
     if fam == MONOEXP:
         g[0:3] = gth * th + 1.0                             # flat prior + log-Jacobian
         lp += float(q[0:3].sum())
+        if prob.theta_prior == 1:                           # Tests/testGamma.R:19-28
+            rate = 1.0 / prob.lambda_scale
+            lp += -rate * float(th.sum())
+            g[0:3] -= rate * th
         return (lp if math.isfinite(lp) else -math.inf), g, sumr2
     # ---- theta ~ multi_normal(theta0, Sigma0)   FitOCT.R:116-117 -------------
     S = np.linalg.inv(prob.Sigma0)

@@ -3,12 +3,14 @@ sampler tests (GPU).  SURVEY.md §8c lists the analytic answers the reference's
 own files imply:
 
 (i)   Tests/testGamma.R:19-47 -- ``lambda ~ exponential(1/lambda_scale)``,
-      lambda_scale = 10, adapt_delta 0.99, max_treedepth 12: mean = sd = 10.
-      Here: normal family with ``prior_PD=1`` and ``lambda_rate=10`` (⚑
-      lambda_conv 0: rate = 1/lambda_rate), whose lambda marginal is exactly that
-      exponential (yGP ~ N(0, lambda) integrates out).  That joint prior is a
-      funnel that biases the lambda marginal a few percent high under NUTS (see
-      check()); its tolerances account for that.
+      lambda_scale = 10, adapt_delta 0.99, max_treedepth 12, 4 chains x (500 warmup
+      + 49,500 draws): mean = sd = 10, median 10 ln 2.  Here at the reference's own
+      settings and precision (gamma_problem / gamma_check): the mono-exponential
+      model with ``theta_prior = 1`` and ``prior_PD = 1`` is exactly that model on each
+      of its three coordinates (include/fitoct.h), with no other parameter to couple
+      to.  (The normal family's lambda has the same exponential marginal, but
+      yGP ~ N(0, lambda) makes the joint prior a funnel whose neck NUTS
+      under-samples by a few percent; its lambda is not used as the known answer.)
 (ii)  Tests/lassoPrior.stan:9-12 -- per-coordinate density
       ``exp(-ls|y| - ls y^2)``; its variance by 1-D quadrature.
 (iii) Tests/horseShoePrior.stan:37-42 with nu = 1 -- z ~ N(0,1),
@@ -87,16 +89,13 @@ def check(family: str, draws: np.ndarray, columns: list, warmup: int, ess_fn):
     mean_check("sigma", hn_mean, hn_sd)
     sd_check("sigma", hn_sd, 0.06)
     if family == "normal":
-        # yGP ~ N(0, lambda) makes (yGP, lambda) a funnel whose neck (small lambda)
-        # NUTS under-samples even at adapt_delta 0.99 (divergences flag it): the
-        # lambda marginal comes out ~5 % high in mean and ~7 % in median, in the
-        # oracle as on the GPU.  Tolerances sized for that known bias.
-        lam = post[:, :, col["lambda"]]
-        if abs(float(lam.mean()) - 10.0) > 1.0:
-            fails.append(f"lambda: mean {float(lam.mean()):.4g} vs 10 (+-10 %)")
-        sd_check("lambda", 10.0, 0.15)
-        quant_check("lambda", 0.5, 10 * math.log(2), 0.15)
-        quant_check("lambda", 0.9, 10 * math.log(10), 0.10)
+        # yGP_k ~ N(0, lambda) given lambda: the standardised yGP / lambda is N(0, 1)
+        # whatever lambda's marginal (the exponential known answer itself is
+        # gamma_check's, without the funnel)
+        for name in [c for c in columns if c.startswith("yGP.")]:
+            zk = post[:, :, col[name]] / post[:, :, col["lambda"]]
+            if abs(float(np.std(zk)) - 1.0) > 0.05:
+                fails.append(f"{name}/lambda: sd {float(np.std(zk)):.4g} vs 1")
     elif family == "lasso":
         sd_t = lasso_sd(10.0)
         for name in [c for c in columns if c.startswith("yGP.")]:
@@ -120,4 +119,40 @@ def check(family: str, draws: np.ndarray, columns: list, warmup: int, ess_fn):
             v = float(np.quantile(lam, q))
             if abs(v - t) > 0.08 * t:
                 fails.append(f"lambda_local.1 q{q} {v:.4g} vs {t:.4g}")
+    return fails
+
+
+# ---- (i) Tests/testGamma.R at its own settings -----------------------------------
+GAMMA_SCALE = 10.0   # testGamma.R:35 lambda_scale
+
+
+def gamma_problem():
+    """testGamma.R's model, ``lambda ~ exponential(1./lambda_scale)`` with lambda_scale =
+    10, on each coordinate of the mono-exponential model (theta_prior = 1, prior_PD = 1:
+    no likelihood, three independent copies)."""
+    d = synth_decay(64, "sincExp", 5)
+    return ExpGPProblem(d["x"], d["y"], d["uy"], prior_type="monoexp", Nn=2,
+                        gridType="extremal", theta0=np.full(3, GAMMA_SCALE), prior_PD=1,
+                        theta_prior=1, lambda_scale=GAMMA_SCALE)
+
+
+def gamma_config(seed=1234):
+    """testGamma.R:42-47: adapt_delta 0.99, max_treedepth 12, warmup 500, iter 50000
+    (warmup included), 4 chains."""
+    return SamplerConfig(chains=4, warmup=500, samples=49_500, seed=seed, adapt_delta=0.99,
+                         max_treedepth=12)
+
+
+def gamma_check(draws, columns, warmup, rtol=0.03):
+    """mean = sd = 10 and median = 10 ln 2 for every theta_k, within ``rtol`` (3 %: at
+    4 x 49,500 draws the Monte-Carlo error of each is ~0.5-1 %)."""
+    post = draws[:, warmup:, :]
+    fails = []
+    for k in range(3):
+        x = post[:, :, columns.index(f"theta.{k + 1}")]
+        for what, v, t in (("mean", float(x.mean()), GAMMA_SCALE),
+                           ("sd", float(x.std()), GAMMA_SCALE),
+                           ("median", float(np.median(x)), GAMMA_SCALE * math.log(2))):
+            if abs(v - t) > rtol * t:
+                fails.append(f"theta.{k + 1}: {what} {v:.5g} vs {t:.5g} (+-{rtol:.0%})")
     return fails

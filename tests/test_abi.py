@@ -277,3 +277,49 @@ def test_device_list_without_gpu_fails_per_device(entry):
         else:
             Batch([_tiny_problem()] * 4, cfg)
     assert ei.value.code == -3 and "device 0" in str(ei.value) and "no HIP device" in str(ei.value)
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(prior_type="normal", theta_prior=1), "mono-exponential model's switch"),
+    (dict(prior_type="monoexp", theta_prior=2), "theta_prior must be 0 or 1"),
+    (dict(prior_type="monoexp", theta_prior=1, lambda_scale=0.0), "lambda_scale"),
+    (dict(prior_type="monoexp", prior_PD=1), "flat prior"),   # improper without theta_prior
+])
+def test_theta_prior_switch_validation(kw, msg):
+    """theta_prior (ABI 5, Tests/testGamma.R's model on the mono-exponential family) is
+    checked before any device work."""
+    from fitoct_amd.api import logp_grad
+    x = np.linspace(20, 500, 16)
+    prob = ExpGPProblem(x, 1000 + 0 * x, 1 + 0 * x, Nn=5, **kw)
+    with pytest.raises(_lib.FitOCTError) as ei:
+        logp_grad(prob, np.zeros((1, prob.D)))
+    assert ei.value.code == -1 and msg in str(ei.value)
+
+
+def test_theta_prior_oracles_agree():
+    """The exponential theta prior in the C oracle and the numpy restatement: lp and
+    gradient agree, and differ from the flat prior by -(1/lambda_scale) sum(theta)."""
+    from oracle import model_np as M
+    from oracle import nuts_c
+    x = np.linspace(20, 500, 16)
+    rng = np.random.default_rng(4)
+    for pd in (0, 1):
+        prob = ExpGPProblem(x, 1000 + 50 * rng.standard_normal(16), 30 + 0 * x, Nn=2,
+                            prior_type="monoexp", theta_prior=1, prior_PD=pd, lambda_scale=10.0,
+                            theta0=np.array([900.0, 1800.0, 250.0]))
+        npp = M.Problem(prob.x, prob.y, prob.uy, Nn=2, family=M.MONOEXP, prior_PD=pd,
+                        theta_prior=1, lambda_scale=10.0, theta0=prob.theta0)
+        flat = M.Problem(prob.x, prob.y, prob.uy, Nn=2, family=M.MONOEXP, prior_PD=pd,
+                         theta0=prob.theta0)
+        q = np.log(prob.theta0) + 0.1 * rng.standard_normal((3, 3))
+        lp_c, g_c, _ = nuts_c.logp_grad(prob, q)
+        for i in range(3):
+            lp_n, g_n, _ = M.logp_grad(q[i], npp)
+            lp_f, g_f, _ = M.logp_grad(q[i], flat)
+            assert lp_c[i] == pytest.approx(lp_n, rel=1e-12, abs=1e-9)
+            np.testing.assert_allclose(g_c[i], g_n, rtol=1e-10, atol=1e-10)
+            th = np.exp(q[i])
+            if pd:   # flat prior + likelihood off: only the Jacobian remains
+                assert lp_n == pytest.approx(q[i].sum() - th.sum() / 10.0, rel=1e-12)
+            else:
+                assert lp_n - lp_f == pytest.approx(-th.sum() / 10.0, rel=1e-10)

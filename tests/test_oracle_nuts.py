@@ -29,6 +29,22 @@ def test_prior_known_answers(family):
     assert max(rh) < (1.05 if family == "normal" else 1.01)
 
 
+def test_testgamma_known_answer_at_reference_precision():
+    """Tests/testGamma.R:19-47 at its own settings (4 chains x 49,500 draws, adapt_delta
+    0.99, max_treedepth 12): lambda ~ exponential(1/10) on each theta_k of the
+    mono-exponential model with theta_prior = 1 -- mean = sd = 10, median 10 ln 2
+    within 3 %, no divergences (no funnel), every chain mixing."""
+    prob = K.gamma_problem()
+    cfg = K.gamma_config()
+    o = nuts_c.sample(prob, cfg, nthreads=4)
+    cols = prob.column_names()
+    fails = K.gamma_check(o["draws"], cols, cfg.warmup)
+    assert not fails, fails
+    post = o["draws"][:, cfg.warmup:, :]
+    assert post[:, :, 5].sum() == 0
+    assert max(diag_np.split_rhat(post[:, :, cols.index(f"theta.{k}")]) for k in (1, 2, 3)) < 1.01
+
+
 def _small(family="normal", N=48, Nn=5):
     from fitoct_amd.synth import default_prior, synth_decay
     t0, S0 = default_prior()
