@@ -46,7 +46,7 @@ def test_struct_layouts_match_ctypes():
     sizes = _lib.struct_sizes()
     assert sizes == (C.sizeof(_lib.Problem), C.sizeof(_lib.Config), C.sizeof(_lib.Result),
                      C.sizeof(_lib.PlanInfo))
-    assert _lib.lib().fitoct_abi_version() == 4 == _lib.ABI_VERSION
+    assert _lib.lib().fitoct_abi_version() == 5 == _lib.ABI_VERSION
 
 
 def test_default_config_is_stan_default():
@@ -60,6 +60,7 @@ def test_default_config_is_stan_default():
     _lib.lib().fitoct_default_problem(C.byref(p))
     assert list(p.theta0) == [1000.0, 2000.0, 300.0] and p.lambda_rate == 0.1
     assert p.Sigma0[0] == pytest.approx(2500.0) and p.Sigma0[1] == 0.0
+    assert p.theta_prior == 0   # ABI 5: the model's own theta prior unless asked
 
 
 @pytest.mark.parametrize("fam", ["normal", "lasso", "horseshoe"])
