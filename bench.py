@@ -412,9 +412,11 @@ def main():
     bufs.clear()
     if (args.config == 3 and n_units == 1 and not args.no_hard and args.adapt_delta == 0.8
             and args.chains == 0 and (W_it, S_it) == (WARMUP_IT, SAMPLES)):
+        # seed of the last timed step (1000 + steps - 1): not a seed chosen by the builder
         line["hard_geometry"] = hard_geometry(prob, C, local, dev, W_it, S_it, cols,
                                               line.get("cpu_baseline"),
-                                              o_means if "cpu_baseline" in line else None)
+                                              o_means if "cpu_baseline" in line else None,
+                                              seed=1000 + args.steps - 1)
     if world > 1 and not args.no_device_list:
         # the route R takes (.Call -> fitoct_config.devices), timed on the same node: rank 0
         # alone drives every GPU of the job from one process while the other ranks wait on
@@ -478,7 +480,7 @@ def device_list_leg(make, devs, draws_per_gpu, dev, flop_per_grad, is_batch=Fals
     return res
 
 
-def hard_geometry(prob, C, local, dev, W_it, S_it, cols, cpu, o_means):
+def hard_geometry(prob, C, local, dev, W_it, S_it, cols, cpu, o_means, seed=1000):
     """The north-star convergence target (max R-hat < 1.01) measured in the same run:
     one config-3 step under the reference's own hard-geometry profile
     (Tests/testGamma.R:45: adapt_delta 0.99, max_treedepth 12; the Shiny app's
@@ -489,7 +491,7 @@ def hard_geometry(prob, C, local, dev, W_it, S_it, cols, cpu, o_means):
     controls), so no second CPU run is needed."""
     import torch
     from fitoct_amd import Plan
-    cfg = make_config(1000, C, 0, local, W_it, S_it, 0.99, 12)
+    cfg = make_config(seed, C, 0, local, W_it, S_it, 0.99, 12)
     with Plan(prob, cfg) as pl:
         buf = torch.empty(pl.info["draws_bytes"] // 8, dtype=torch.float64, device=dev)
         stream = torch.cuda.current_stream(dev)
@@ -505,7 +507,7 @@ def hard_geometry(prob, C, local, dev, W_it, S_it, cols, cpu, o_means):
     conv = convergence(out.draws, out.warmup_saved, cols)
     res = {"workload": (f"fitExpGP+horseshoe N={N_BINS} Nn={NN} {C} chains W={W_it} S={S_it} "
                         "adapt_delta=0.99 max_treedepth=12 (Tests/testGamma.R:45)"),
-           "seed": 1000, "value": round(value, 2), "unit": "draws/s",
+           "seed": seed, "value": round(value, 2), "unit": "draws/s",
            "ms_per_step": round(wall * 1e3, 2), "kernel_ms": round(kms, 2),
            "gradients_per_launch": lf,
            "gradients_per_iteration": round(lf / (C * (W_it + S_it)), 1),

@@ -429,11 +429,12 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   // four chains per tile -- the headline shape -- sweeps 16 bins per lane over half the
   // gradient waves per chain, so the per-sweep reduction and set-up are paid once per 16
   // bins.  The bins are staged as before (n_pad = 2048 either way); only the lane stride
-  // (128) and the geometric-grid factors change.  Sampler plans only (the logp kernel
-  // keeps whole tiles); opt-in with FITOCT_SPLIT=1 while it is measured.
+  // (128) and the geometric-grid factors change.  The logp kernel follows the same split
+  // (so the lp / gradient parity tests exercise this sweep); opt-in with FITOCT_SPLIT=1
+  // while it is measured.
   k.gsplit = 1;
   double Rs[24];
-  if (max_depth > 0 && force_bpt < 0 && G == GMAX && pl->bpt == 8 && k.mode == MODE_POLY &&
+  if (force_bpt < 0 && G == GMAX && pl->bpt == 8 && k.mode == MODE_POLY &&
       !pl->mixed && p->prior_type != FITOCT_MODEL_MONOEXP && p->N > 4 * GT &&
       getenv("FITOCT_SPLIT") != nullptr && getenv("FITOCT_NO_GEO") == nullptr &&
       geo_ratios(p, pl->nnp, 16, Rs, GT / 2)) {

@@ -2879,9 +2879,13 @@ __global__ void __launch_bounds__(TPB, 2) logp_kernel(const KParams* __restrict_
   }
   __syncthreads();
   if (wave < NGW && P.prior_PD == 0) {
+    // split tile (P.gsplit = 2): gradient waves {0,1} sweep points {0,1}, {2,3} points {2,3}
+    const int gwpc = NGW / P.gsplit, grp = wave / gwpc, per = GMAX / P.gsplit;
     Bins<R, BPT, NNP, MODE> bins;
-    bins.load(P, tid, GT);   // the logp kernel never splits its tile
-    gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), done, 0, nct, tid, lane, wave);
+    bins.load(P, (wave % gwpc) * WAVE + lane, GT / P.gsplit);
+    gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), done, grp * per,
+                                     min(nct, (grp + 1) * per), (wave % gwpc) * WAVE + lane,
+                                     lane, wave % gwpc);
   }
   __syncthreads();
   if (wave >= NGW && c < nct) {

@@ -121,3 +121,61 @@ def test_non_physical_guard_and_many_points():
     assert np.all(lp[::7] == -np.inf)
     sel = rng.choice(3000, 40, replace=False)
     _check(lp[sel], g[sel], s2[sel], npp, Q[sel], "f64")
+
+
+@pytest.mark.parametrize("fam", ["horseshoe", "normal"])
+def test_split_tile_sweep(fam, monkeypatch):
+    """The split tile (kernel_params.h gsplit: N in (1024, 2048] with four points per tile,
+    16 bins per lane over two gradient waves per point, lane stride 128, FITOCT_SPLIT=1):
+    lp / gradient at the f64 tolerances against the numpy oracle, at the headline shape
+    (N = 2048) and a ragged one (N = 1500), on 1100 points so that every tile holds four."""
+    t0, S0 = default_prior()
+    rng = np.random.default_rng(17)
+    for N in (2048, 1500):
+        d = synth_decay(N, "sincExp", 1234)
+        prob = ExpGPProblem(d["x"], d["y"], d["uy"], Nn=15, gridType="extremal", theta0=t0,
+                            Sigma0=S0, prior_type=fam)
+        npp = M.Problem(d["x"], d["y"], d["uy"], Nn=15, grid_type="extremal", theta0=t0,
+                        Sigma0=S0, family=M.FAMILIES[fam])
+        Q = _points(prob, rng, P=1100, spread=0.2)
+        monkeypatch.setenv("FITOCT_SPLIT", "1")
+        lp, g, s2 = logp_grad(prob, Q, "f64")
+        monkeypatch.delenv("FITOCT_SPLIT")
+        lp0, g0, _ = logp_grad(prob, Q, "f64")
+        sel = rng.choice(1100, 40, replace=False)
+        _check(lp[sel], g[sel], s2[sel], npp, Q[sel], "f64")
+        np.testing.assert_allclose(lp, lp0, rtol=1e-11, atol=1e-9)   # split vs 8-bin layout
+        np.testing.assert_allclose(g, g0, rtol=1e-8, atol=1e-8)
+
+
+def test_large_y_over_uy_conditioning():
+    """Rounding of the staged residual: the kernel stages y / uy per bin and
+    forms (y - m) / uy as fma(-m, 1/uy, y/uy); the oracles compute (y - m) * (1/uy).  Both
+    are exact to a few ulps of y/uy, so with |y/uy| ~ 4e6 and residuals ~ 1 each residual
+    carries ~1e-9 absolute error whichever form is used.  The tolerances below are the
+    1e-11 / 1e-8 of the other tests plus that conditioning term: 8 eps sum |d_i| |y_i/uy_i|
+    on lp (d_i = residual), and the same amplification (|y/uy| / |d|) on the gradient."""
+    t0 = np.array([2.0e6, 3000.0, 300.0])
+    x = np.linspace(20.0, 500.0, 512)
+    uy = np.full(512, 0.5)
+    rng = np.random.default_rng(5)
+    y = t0[0] + t0[1] * np.exp(-2.0 * x / t0[2]) + uy * rng.standard_normal(512)
+    S0 = np.diag((0.05 * t0) ** 2)
+    prob = ExpGPProblem(x, y, uy, Nn=10, gridType="extremal", theta0=t0, Sigma0=S0,
+                        prior_type="normal")
+    npp = M.Problem(x, y, uy, Nn=10, grid_type="extremal", theta0=t0, Sigma0=S0)
+    Q = np.zeros((6, prob.D))
+    Q[:, 0:3] = np.log(t0) + rng.normal(0, 1e-7, (6, 3))   # residuals O(1)
+    Q[:, 3:13] = rng.normal(0, 1e-4, (6, 10))
+    Q[:, 13] = np.log(0.1)
+    lp, g, _ = logp_grad(prob, Q, "f64")
+    eps = np.finfo(float).eps
+    for i, q in enumerate(Q):
+        rl, rg, _ = M.logp_grad(q, npp)
+        th = np.exp(q[:3])
+        d = (y - (th[0] + th[1] * np.exp(-2.0 * x / th[2]))) / uy
+        kappa = float(np.median(np.abs(y / uy)) / max(np.median(np.abs(d)), 1e-300))
+        tol = 1e-11 * (1 + abs(rl)) + 8 * eps * float(np.sum(np.abs(d) * np.abs(y / uy)))
+        assert abs(lp[i] - rl) <= tol, (i, lp[i], rl, tol)
+        err = np.abs(g[i] - rg) / (1 + np.abs(rg))
+        assert err.max() <= 1e-8 * max(1.0, kappa), (i, err.max(), kappa)
