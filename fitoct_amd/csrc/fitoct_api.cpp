@@ -247,7 +247,7 @@ bool build_poly(const fitoct_problem* p, const std::vector<double>& B, int nnp,
 // in i), which lets the sweep form a lane's moments by Horner in R^l
 // (nuts_device.hip moments_geo).  Accepted only if every x_i lies on the line
 // through x_0 and x_{N-1} to 1e-12 of the range and no (R^l)^b can overflow.
-bool geo_ratios(const fitoct_problem* p, int nnp, int bpt, double* R, int stride = GT) {
+bool geo_ratios(const fitoct_problem* p, int nnp, int bpt, double* R) {
   const int N = p->N, Nn = p->Nn;
   if (bpt < 2 || Nn < 2) return false;
   double xmin = p->x[0], xmax = p->x[0];
@@ -262,7 +262,7 @@ bool geo_ratios(const fitoct_problem* p, int nnp, int bpt, double* R, int stride
   const double s2 = (p->kernel_conv == 0) ? rho * rho : 0.5 * rho * rho;
   const double dg = (p->grid_type == FITOCT_GRID_INTERNAL) ? (1.0 - 1.0 / (Nn + 1)) / (Nn - 1)
                                                            : 1.0 / (Nn - 1);
-  const double logR = stride * (step / range) * dg / s2;
+  const double logR = GT * (step / range) * dg / s2;
   if (fabs(logR) * (nnp - 1) * (bpt - 1) > 600.0) return false;
   if (bpt == 16) {   // c*x_b and t_b are formed in the kernel: x must be on the line to ~ulps
     for (int i = 0; i < N; ++i)
@@ -425,28 +425,6 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
     return fail(FITOCT_E_ARG, "max_treedepth too large for the LDS budget");
   k.G = G;
   k.max_depth = max_depth;
-  // Split tile (kernel_params.h gsplit): N in (1024, 2048] on an arithmetic depth grid with
-  // four chains per tile -- the headline shape -- sweeps 16 bins per lane over half the
-  // gradient waves per chain, so the per-sweep reduction and set-up are paid once per 16
-  // bins.  The bins are staged as before (n_pad = 2048 either way); only the lane stride
-  // (128) and the geometric-grid factors change.  The logp kernel follows the same split
-  // (so the lp / gradient parity tests exercise this sweep); opt-in with FITOCT_SPLIT=1
-  // while it is measured.
-  k.gsplit = 1;
-  double Rs[24];
-  if (force_bpt < 0 && G == GMAX && pl->bpt == 8 && k.mode == MODE_POLY &&
-      !pl->mixed && p->prior_type != FITOCT_MODEL_MONOEXP && p->N > 4 * GT &&
-      getenv("FITOCT_SPLIT") != nullptr && getenv("FITOCT_NO_GEO") == nullptr &&
-      geo_ratios(p, pl->nnp, 16, Rs, GT / 2)) {
-    k.gsplit = 2;
-    pl->bpt = 16;
-    for (int l = 0; l < 24; ++l) k.geo_R[l] = Rs[l];
-    k.geo = 1;
-    const double cstep = (double)p->data_type * (p->x[p->N - 1] - p->x[0]) / (p->N - 1);
-    for (int b = 0; b < 16; ++b) k.geo_dcx[b] = (double)b * (GT / 2) * cstep;
-    k.geo_tmax = 0.0;
-    for (int i = 0; i < p->N; ++i) k.geo_tmax = std::max(k.geo_tmax, ta[2 * (size_t)i]);
-  }
   k.nuts_prio = getenv("FITOCT_NUTS_PRIO") ? atoi(getenv("FITOCT_NUTS_PRIO")) : 3;
   k.spec = 0;   // set below, once migration is decided
   pl->tiles = (chains + G - 1) / G;

@@ -72,10 +72,6 @@ struct KParams {
   int chains;               // chains in this launch
   int chain_offset;         // global id of chain 0
   int G;                    // chains per tile
-  // 1, or 2 = split tile: gradient waves {0,1} sweep chain slots {0,1} and waves {2,3}
-  // slots {2,3}, each pair over every bin, bins strided over 128 lanes (16 per lane, the
-  // compact layout): one cross-lane reduction per 16 bins instead of per 8
-  int gsplit;
   int warmup, samples, max_depth, save_warmup, adapt;
   uint64_t seed;
   double adapt_delta, gamma, kappa, t0, stepsize0, init_radius;

@@ -677,8 +677,7 @@ struct Bins {
   static constexpr int NR = MODE == MODE_POLY ? 2 : NNP;
   R cx[NB], y[NB], isu[NB];
   R row[NB][NR];
-  // bins tid + b * stride (stride = GT, or GT / 2 in a split tile)
-  __device__ void load(KPc& P, int tid, int stride) {
+  __device__ void load(KPc& P, int tid) {
     if constexpr (BPT > 0) {
       const AS_GLB R* pcx = (const AS_GLB R*)P.cx;
       const AS_GLB R* py = (const AS_GLB R*)P.y;
@@ -689,7 +688,7 @@ struct Bins {
         row[0][0] = pB[2 * (size_t)tid];
 #pragma unroll
         for (int b = 0; b < BPT; ++b) {
-          const int i = tid + b * stride;
+          const int i = tid + b * GT;
           y[b] = py[i];
           isu[b] = pisu[i];
           row[b][1] = pB[2 * (size_t)i + 1];
@@ -697,7 +696,7 @@ struct Bins {
       } else {
 #pragma unroll
         for (int b = 0; b < BPT; ++b) {
-          const int i = tid + b * stride;
+          const int i = tid + b * GT;
           cx[b] = pcx[i];
           y[b] = py[i];
           isu[b] = pisu[i];
@@ -1219,10 +1218,8 @@ struct Chain {
     if (lik) {
       double sl = 0.0;
       if (lane < 4 + NNP) {
-        const int gw = NGW / Pr().gsplit;   // gradient waves that swept this chain
 #pragma unroll
-        for (int w = 0; w < NGW; ++w)
-          if (w < gw) sl += part[(slot * NGW + w) * NSLOT + lane];
+        for (int w = 0; w < NGW; ++w) sl += part[(slot * NGW + w) * NSLOT + lane];
         if (poly && lane >= 4) sl *= bv[lane - 4];   // b .* M  (B^T h = K^-1 (b .* M))
         SUMS[lane] = sl;
       }
@@ -2460,11 +2457,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nct = min(P.G, P.chains - c0);
-  // one hand-off ring per gradient group: the tile's, or each half's in a split tile
-  // (chain slot c -> group c / (GMAX / gsplit), gradient waves w -> group w / gwpc)
-  __shared__ unsigned long long ring[2 * RINGN];
-  __shared__ int q_reserve[2], n_active, grad_cnt[GMAX];
-  const int gsplit = P.gsplit, gwpc = NGW / gsplit;   // gradient waves per chain
+  __shared__ unsigned long long ring[RINGN];
+  __shared__ int q_reserve, n_active, grad_cnt[GMAX];
   __shared__ long long done_t[GMAX];   // profiling build: when the 8th wave finished chain c
   __shared__ long long start_min[GMAX], start_max[GMAX];
   // speculative leaves (P.spec, one chain per tile): the chain's NUTS wave posts a
@@ -2477,8 +2471,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
 
   load_kinv<PPL, NNP>(P, L, tid);
   if (tid == 0) {
-    q_reserve[0] = 0;
-    q_reserve[1] = 0;
+    q_reserve = 0;
     n_active = nct;
     live_chains = nct;
     help_req = 0;
@@ -2492,7 +2485,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     start_min[tid] = 0x7FFFFFFFFFFFFFFFLL;
     start_max[tid] = 0;
   }
-  if (tid < 2 * RINGN) ring[tid] = ~0ULL;
+  if (tid < RINGN) ring[tid] = ~0ULL;
   if (MIG && P.mig != nullptr) {   // every slot of the tile may host migrants: all NUTS waves live
     if (tid == 0) {
       const MigView M(P.mig, P.mig_tiles);
@@ -2520,10 +2513,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   }
   if (kProfile) __syncthreads();
   if (wave < NGW) {  // ------------------------- gradient waves
-    const int grp = wave / gwpc, wsub = wave % gwpc, gtid = wsub * WAVE + lane;
-    unsigned long long* gring = ring + grp * RINGN;
     Bins<R, BPT, NNP, MODE> bins;
-    bins.load(P, gtid, GT / gsplit);
+    bins.load(P, tid);
     int zero_done[GMAX] = {0, 0, 0, 0};
     unsigned long long t_idle = 0;
     for (unsigned h = 0;; ++h) {
@@ -2531,7 +2522,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       bool stop = false;
       long long spins = 0;
       for (;;) {  // wait for ring entry h
-        e = lds_load64(&gring[h % RINGN]);
+        e = lds_load64(&ring[h % RINGN]);
         if ((unsigned)(e >> 32) == h) break;
         if (lds_load(&n_active) == 0) {
           stop = true;
@@ -2563,8 +2554,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         atomicMax((unsigned long long*)&start_max[c], t);
       }
       if (P.prior_PD == 0)
-        gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1, gtid,
-                                         lane, wsub);
+        gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1, tid,
+                                         lane, wave);
       wave_fence();   // this wave's PART writes are complete
       if (wstamp) t_wbusy += (long long)__builtin_amdgcn_s_memtime() - s0w;
       if (lane == 0) {
@@ -2588,8 +2579,6 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     }
     const int c = wave - NGW;
     const bool mig = MIG && P.mig != nullptr;
-    const int grp = c / (GMAX / gsplit);   // this slot's gradient group (its ring)
-    unsigned long long* gring = ring + grp * RINGN;
     if (helped && c == 1) {   // the helper wave of slot 0's chain
       using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
       Ch ch(P, L, 0, c0, lane, nct);
@@ -2635,7 +2624,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     }
     if (c < (mig ? P.G : nct)) {
       using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
-      long long epoch = 0;     // this slot's hand-offs (grad_cnt[c] counts gwpc per epoch)
+      long long epoch = 0;     // this slot's hand-offs (grad_cnt[c] counts NGW per epoch)
       int lc = c < nct ? c0 + c : -1;
       int a = Ch::A_INIT_STATE;
       for (;;) {   // the slot's own chain, then (migration) chains handed over by other tiles
@@ -2657,8 +2646,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             continue;
           }
           if (lane == 0) {
-            const unsigned slot = (unsigned)atomicAdd(&q_reserve[grp], 1);
-            __atomic_store_n(&gring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
+            const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
+            __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
                              __ATOMIC_RELAXED);
             if (ch.deep) {
               wave_fence();   // the hand-off (HX) lands before the request number
@@ -2695,7 +2684,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           long long spins = 0;
           const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
           if (stamp) t_busy += w0 - s0;
-          while (lds_load(&grad_cnt[c]) < (int)(gwpc * epoch) || lds_load(&help_done) < hreq) {
+          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch) || lds_load(&help_done) < hreq) {
             if (++spins > SPIN_LIMIT) break;
             __builtin_amdgcn_s_sleep(1);
           }
@@ -2729,13 +2718,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           // rarely, so the waiting wave leaves the SIMD's issue to the gradient wave.
           if (P.G >= 2 && (BPT >= 8 || BPT == 0)) {
             if (FITOCT_NUTS_WAIT_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_NUTS_WAIT_PRIO);
-            while (lds_load(&grad_cnt[c]) < (int)(gwpc * epoch)) {
+            while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
               if (++spins > SPIN_LIMIT) break;
               __builtin_amdgcn_s_sleep(FITOCT_NUTS_POLL);
             }
             if (FITOCT_NUTS_WAIT_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
           } else {
-            while (lds_load(&grad_cnt[c]) < (int)(gwpc * epoch)) {
+            while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
               if (++spins > SPIN_LIMIT) break;
               __builtin_amdgcn_s_sleep(1);
             }
@@ -2782,12 +2771,12 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           if (P.bench_sweeps > 0 && P.stamps != nullptr) {   // sweep-only measurement
             for (int r = 0; r < P.bench_sweeps; ++r) {
               if (lane == 0) {
-                const unsigned slot = (unsigned)atomicAdd(&q_reserve[grp], 1);
-                __atomic_store_n(&gring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
+                const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
+                __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
                                  __ATOMIC_RELAXED);
               }
               ++epoch;
-              while (lds_load(&grad_cnt[c]) < (int)(gwpc * epoch)) __builtin_amdgcn_s_sleep(1);
+              while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) __builtin_amdgcn_s_sleep(1);
             }
             ch.Sp->state = ST_DONE;
             break;
@@ -2795,8 +2784,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         }
         // enqueue chain c: sequence number from a ring-wide counter, one 64-bit store
         if (lane == 0) {
-          const unsigned slot = (unsigned)atomicAdd(&q_reserve[grp], 1);
-          __atomic_store_n(&gring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
+          const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
+          __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
                            __ATOMIC_RELAXED);
         }
         if (stamp) t_enq = (long long)__builtin_amdgcn_s_memtime();
@@ -2879,13 +2868,9 @@ __global__ void __launch_bounds__(TPB, 2) logp_kernel(const KParams* __restrict_
   }
   __syncthreads();
   if (wave < NGW && P.prior_PD == 0) {
-    // split tile (P.gsplit = 2): gradient waves {0,1} sweep points {0,1}, {2,3} points {2,3}
-    const int gwpc = NGW / P.gsplit, grp = wave / gwpc, per = GMAX / P.gsplit;
     Bins<R, BPT, NNP, MODE> bins;
-    bins.load(P, (wave % gwpc) * WAVE + lane, GT / P.gsplit);
-    gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), done, grp * per,
-                                     min(nct, (grp + 1) * per), (wave % gwpc) * WAVE + lane,
-                                     lane, wave % gwpc);
+    bins.load(P, tid);
+    gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), done, 0, nct, tid, lane, wave);
   }
   __syncthreads();
   if (wave >= NGW && c < nct) {

@@ -123,31 +123,6 @@ def test_non_physical_guard_and_many_points():
     _check(lp[sel], g[sel], s2[sel], npp, Q[sel], "f64")
 
 
-@pytest.mark.parametrize("fam", ["horseshoe", "normal"])
-def test_split_tile_sweep(fam, monkeypatch):
-    """The split tile (kernel_params.h gsplit: N in (1024, 2048] with four points per tile,
-    16 bins per lane over two gradient waves per point, lane stride 128, FITOCT_SPLIT=1):
-    lp / gradient at the f64 tolerances against the numpy oracle, at the headline shape
-    (N = 2048) and a ragged one (N = 1500), on 1100 points so that every tile holds four."""
-    t0, S0 = default_prior()
-    rng = np.random.default_rng(17)
-    for N in (2048, 1500):
-        d = synth_decay(N, "sincExp", 1234)
-        prob = ExpGPProblem(d["x"], d["y"], d["uy"], Nn=15, gridType="extremal", theta0=t0,
-                            Sigma0=S0, prior_type=fam)
-        npp = M.Problem(d["x"], d["y"], d["uy"], Nn=15, grid_type="extremal", theta0=t0,
-                        Sigma0=S0, family=M.FAMILIES[fam])
-        Q = _points(prob, rng, P=1100, spread=0.2)
-        monkeypatch.setenv("FITOCT_SPLIT", "1")
-        lp, g, s2 = logp_grad(prob, Q, "f64")
-        monkeypatch.delenv("FITOCT_SPLIT")
-        lp0, g0, _ = logp_grad(prob, Q, "f64")
-        sel = rng.choice(1100, 40, replace=False)
-        _check(lp[sel], g[sel], s2[sel], npp, Q[sel], "f64")
-        np.testing.assert_allclose(lp, lp0, rtol=1e-11, atol=1e-9)   # split vs 8-bin layout
-        np.testing.assert_allclose(g, g0, rtol=1e-8, atol=1e-8)
-
-
 def test_large_y_over_uy_conditioning():
     """Rounding of the staged residual: the kernel stages y / uy per bin and
     forms (y - m) / uy as fma(-m, 1/uy, y/uy); the oracles compute (y - m) * (1/uy).  Both
