@@ -152,14 +152,18 @@ def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, adapt_delta=0.8, max_tre
 def convergence(draws, W_saved, cols):
     """Split and rank-normalised R-hat of the post-warmup draws over the parameter
     columns (theta, z / yGP, the scales, sigma, br; the horseshoe's inverse-gamma
-    auxiliaries r2_* excluded), with and without the funnel-trapped chains (divergence
-    rate > 50 %), and the three worst columns by name."""
+    auxiliaries r2_* excluded), with and without the funnel-trapped chains, and the three
+    worst columns by name.  A chain counts as trapped when more than half of its
+    transitions diverge over the run or over either half of it (a chain can fall into the
+    funnel's neck mid-run: seed 1019 at the hard-geometry profile)."""
     from fitoct_amd.stanfit import rank_rhat, split_rhat_ess
     post = draws[:, W_saved:, :]
     par = [j for j, n in enumerate(cols) if j >= 7 and not n.startswith("r2_")]
     rh = {cols[j]: split_rhat_ess(post[:, :, j])[0] for j in par}
     rrh = {cols[j]: rank_rhat(post[:, :, j]) for j in par}   # Vehtari et al. 2021
-    stuck = post[:, :, 5].mean(1) > 0.5
+    h = post.shape[1] // 2
+    stuck = ((post[:, :, 5].mean(1) > 0.5) | (post[:, :h, 5].mean(1) > 0.5)
+             | (post[:, h:, 5].mean(1) > 0.5))
     free = post[~stuck]
     rh_free = {cols[j]: split_rhat_ess(free[:, :, j])[0] for j in par} if stuck.any() else rh
     rrh_free = {cols[j]: rank_rhat(free[:, :, j]) for j in par} if stuck.any() else rrh
