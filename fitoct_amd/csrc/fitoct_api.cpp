@@ -1060,6 +1060,19 @@ int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
     std::vector<int> st(C);
     HIP_TRY(hipMemcpy(st.data(), k.chain_status, sizeof(int) * C, hipMemcpyDeviceToHost));
     if (res->chain_status) memcpy(res->chain_status, st.data(), sizeof(int) * C);
+    // A chain that timed out may have left a speculative booking in flight while it wrote
+    // its final state, so its warm-restart outputs could be torn: they are reported as NaN
+    // (fitoct_plan_set_init rejects them).  Done here, not in the kernel: any code added to
+    // the sampler's finishing action moved the headline kernel's layout and cost 2 %
+    // (profiles/r04_ab_regression.txt).
+    for (int c = 0; c < C; ++c)
+      if (st[c] == FITOCT_E_TIMEOUT) {
+        if (res->stepsize) res->stepsize[c] = NAN;
+        for (int j = 0; j < D; ++j) {
+          if (res->inv_metric) res->inv_metric[(size_t)c * D + j] = NAN;
+          if (res->last_q) res->last_q[(size_t)c * D + j] = NAN;
+        }
+      }
     std::vector<long long> lf(C);
     HIP_TRY(hipMemcpy(lf.data(), k.leapfrogs, sizeof(long long) * C, hipMemcpyDeviceToHost));
     long long tot = 0;

@@ -67,7 +67,6 @@ struct KParams {
   double nu;                // horseshoe nu
   double sigma_scale;
   double sigma_scale_inv;   // 1 / sigma_scale
-  double theta_rate;        // mono-exp, theta_prior = 1: theta_k ~ exponential(theta_rate)
   // ---- sampler ----
   int chains;               // chains in this launch
   int chain_offset;         // global id of chain 0
@@ -111,6 +110,8 @@ struct KParams {
   double* lp_out;           // [points]
   double* grad_out;         // [points][D]
   double* s2_out;           // [points]
+  // appended (ABI 5), so the offsets of every field above are those of round 3
+  double theta_rate;        // mono-exp, theta_prior = 1: theta_k ~ exponential(theta_rate)
 };
 
 }  // namespace fitoct

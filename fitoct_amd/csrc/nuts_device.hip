@@ -2278,22 +2278,17 @@ struct Chain {
   __device__ int act_finish() {
     FITOCT_MARK(act_finish);
     Sp->state = ST_DONE;
-    // A chain that timed out may have left a speculative booking in flight, which can still
-    // be writing the sample / metric vectors: its warm-restart outputs are NaN, never torn
-    // values (fitoct_plan_set_init rejects them)
-    const double bad = (uni(Sp->status) == ERR_TIMEOUT) ? __builtin_nan("") : 0.0;
     const V q = ld(V_SMP_Q), minv = ld(V_MINV);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
       const int k = idx(s);
       if (k < Pr().D) {
-        if (Pr().fin_q) ((AS_GLB double*)Pr().fin_q)[(size_t)lc * Pr().D + k] = q.a[s] + bad;
-        if (Pr().fin_minv)
-          ((AS_GLB double*)Pr().fin_minv)[(size_t)lc * Pr().D + k] = minv.a[s] + bad;
+        if (Pr().fin_q) ((AS_GLB double*)Pr().fin_q)[(size_t)lc * Pr().D + k] = q.a[s];
+        if (Pr().fin_minv) ((AS_GLB double*)Pr().fin_minv)[(size_t)lc * Pr().D + k] = minv.a[s];
       }
     }
     if (lane == 0) {
-      if (Pr().fin_eps) ((AS_GLB double*)Pr().fin_eps)[lc] = Sp->eps + bad;
+      if (Pr().fin_eps) ((AS_GLB double*)Pr().fin_eps)[lc] = Sp->eps;
       if (Pr().chain_status) ((AS_GLB int*)Pr().chain_status)[lc] = Sp->status;
       if (Pr().leapfrogs) ((AS_GLB long long*)Pr().leapfrogs)[lc] = Sp->leapfrogs;
     }
