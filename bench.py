@@ -159,7 +159,9 @@ def convergence(draws, W_saved, cols):
     from fitoct_amd.stanfit import rank_rhat, split_rhat_ess
     post = draws[:, W_saved:, :]
     par = [j for j, n in enumerate(cols) if j >= 7 and not n.startswith("r2_")]
-    rh = {cols[j]: split_rhat_ess(post[:, :, j])[0] for j in par}
+    rhe = {cols[j]: split_rhat_ess(post[:, :, j]) for j in par}
+    rh = {k: v[0] for k, v in rhe.items()}
+    ess = {k: v[1] for k, v in rhe.items()}   # rstan n_eff over all chains
     rrh = {cols[j]: rank_rhat(post[:, :, j]) for j in par}   # Vehtari et al. 2021
     h = post.shape[1] // 2
     stuck = ((post[:, :, 5].mean(1) > 0.5) | (post[:, :h, 5].mean(1) > 0.5)
@@ -175,7 +177,12 @@ def convergence(draws, W_saved, cols):
             "rank_rhat_max": round(max(rrh.values()), 5),
             "rank_rhat_max_excl_stuck": round(max(rrh_free.values()), 5),
             "divergent_frac": round(float(post[:, :, 5].mean()), 5),
-            "rhat_worst_columns": worst(rh), "rank_rhat_worst_columns": worst(rrh)}
+            "rhat_worst_columns": worst(rh), "rank_rhat_worst_columns": worst(rrh),
+            # slow mixing vs trapping: with nothing trapped, split R-hat - 1 ~ 1 / (bulk ESS
+            # per chain), e.g. config 4's yGP.6-8 (~90 per 1000 draws)
+            "ess_per_chain_min": round(min(ess.values()) / post.shape[0], 1),
+            "ess_per_chain_lowest_columns": [[k, round(v / post.shape[0], 1)] for k, v in
+                                             sorted(ess.items(), key=lambda t: t[1])[:3]]}
 
 
 def load_traffic(workload):
