@@ -435,10 +435,13 @@ def main():
         hb = dist.new_group(backend="gloo")
         dist.barrier(group=hb)
         if rank == 0:
-            line["device_list"] = device_list_leg(
-                lambda step, devs: Plan(prob, _dl_config(args, C * len(devs), W_it, S_it,
-                                                         step, devs)),
-                _dl_devices(world), C * S_it, dev, f_grad(N_bins, NN))
+            try:   # a side measurement: it must not cost the headline line
+                line["device_list"] = device_list_leg(
+                    lambda step, devs: Plan(prob, _dl_config(args, C * len(devs), W_it, S_it,
+                                                             step, devs)),
+                    _dl_devices(world), C * S_it, dev, f_grad(N_bins, NN))
+            except Exception as e:   # noqa: BLE001
+                line["device_list"] = {"error": f"{type(e).__name__}: {e}"}
         dist.barrier(group=hb)
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -675,10 +678,14 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it, 
         hb = dist.new_group(backend="gloo")   # host barrier: no collective kernel on the GPUs
         dist.barrier(group=hb)
         if rank == 0:
-            every = file_problems(0, conf["files"])
-            line["device_list"] = device_list_leg(
-                lambda step, devs: batch_for(step, every, 0, devs), _dl_devices(world),
-                conf["files"] // world * C * S_it, dev, f_grad(conf["N"], NN), is_batch=True)
+            try:   # a side measurement: it must not cost the main line
+                every = file_problems(0, conf["files"])
+                line["device_list"] = device_list_leg(
+                    lambda step, devs: batch_for(step, every, 0, devs), _dl_devices(world),
+                    conf["files"] // world * C * S_it, dev, f_grad(conf["N"], NN),
+                    is_batch=True)
+            except Exception as e:   # noqa: BLE001
+                line["device_list"] = {"error": f"{type(e).__name__}: {e}"}
         dist.barrier(group=hb)
     if rank == 0:
         print(json.dumps(line), flush=True)
