@@ -34,3 +34,28 @@ def test_device_list_arguments(args, env, msg):
     r = _bench(*args, env=env)
     assert r.returncode != 0
     assert msg in (r.stderr + r.stdout), r.stderr[-2000:]
+
+
+def test_convergence_counts_chains_trapped_mid_run():
+    """bench.convergence's trapped rule (DESIGN.md §7): more than half of a chain's
+    transitions divergent over the run OR over either half of it -- a chain that falls
+    into the funnel mid-run (seed 1019 at the hard-geometry profile: 96 % of its
+    second-half transitions diverge, 48 % over the run) is counted; R-hat is reported
+    with and without such chains, and per-chain bulk ESS next to it."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    rng = np.random.default_rng(0)
+    C, W, S = 40, 10, 400
+    cols = ["lp__", "accept_stat__", "stepsize__", "treedepth__", "n_leapfrog__",
+            "divergent__", "energy__", "theta.1", "theta.2"]
+    d = np.zeros((C, W + S, len(cols)))
+    d[:, :, 7:] = rng.standard_normal((C, W + S, 2))
+    d[3, W + S // 2:, 5] = 1.0           # chain 3 diverges on its whole second half
+    d[3, W + S // 2:, 7] = 8.0           # ... stuck far from the bulk
+    d[5, W:, 5] = (rng.random(S) < 0.45).astype(float)   # 45 % everywhere: not trapped
+    out = bench.convergence(d, W, cols)
+    assert out["stuck_chains"] == 1
+    assert out["rhat_max"] > 1.1 and out["rhat_max_excl_stuck"] < 1.02
+    assert out["ess_per_chain_min"] > 0
+    assert [c for c, _ in out["ess_per_chain_lowest_columns"]][:1] in (["theta.1"], ["theta.2"])
