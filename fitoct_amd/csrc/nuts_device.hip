@@ -69,6 +69,13 @@ enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2, FAM_MONO = 3 };
 #ifndef FITOCT_PAIRED_BINS
 #define FITOCT_PAIRED_BINS 1
 #endif
+// Sweeps of at most 2 bins per lane (N <= 512: configs 2 and 5) are latency-bound (two
+// independent bins per lane, then the reduction): the basis polynomial and exp are then
+// evaluated by Estrin's scheme (dependency depth 4-5 instead of 12-14, three more
+// multiplies).  FITOCT_LAT_SWEEP=0 builds the Horner forms there too (A/B).
+#ifndef FITOCT_LAT_SWEEP
+#define FITOCT_LAT_SWEEP 1
+#endif
 // 16 bins per lane (config 4): bins in groups of FITOCT_BPT16_GROUP whose moments are
 // formed per group, and (FITOCT_BPT16_PAIRS) pairs sharing one reciprocal
 #ifndef FITOCT_BPT16_GROUP
@@ -431,6 +438,42 @@ template <> __device__ __forceinline__ double exp_<double>(double x) {
   return ldexp(p, ni);
 }
 template <> __device__ __forceinline__ float exp_<float>(float x) { return __expf(x); }
+
+// Estrin's scheme for sum_k c[k] t^k (k < N): pairs c[2j] + c[2j+1] t, then pairs of those
+// with t^2, t^4, ...: dependency depth ceil(log2 N) + 1 FMAs instead of N - 1.
+template <int N>
+__device__ __forceinline__ double estrin(const double* c, double t) {
+  constexpr int M = (N + 1) / 2;
+  double v[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) v[j] = (2 * j + 1 < N) ? fma(c[2 * j + 1], t, c[2 * j]) : c[2 * j];
+  double x = t * t;
+#pragma unroll
+  for (int n = M; n > 1; n = (n + 1) / 2) {
+#pragma unroll
+    for (int j = 0; j < n / 2; ++j) v[j] = fma(v[2 * j + 1], x, v[2 * j]);
+    if (n & 1) v[n / 2] = v[n - 1];
+    x = x * x;
+  }
+  return v[0];
+}
+// exp_<double>'s reduction and Taylor-12 polynomial, the polynomial by Estrin
+__device__ __forceinline__ double exp_lat(double x) {
+  x = fmax(x, -746.0);
+  const double SH = 6755399441055744.0;   // 1.5 * 2^52
+  const double t = fma(x, 1.4426950408889634, SH);
+  const double n = t - SH;
+  const int ni = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
+  double r = fma(-n, 6.93147180369123816490e-01, x);
+  r = fma(-n, 1.90821492927058770002e-10, r);
+  constexpr double c[13] = {1.0, 1.0, 0.5, 1.66666666666666666667e-01,
+                            4.16666666666666666667e-02, 8.33333333333333333333e-03,
+                            1.38888888888888888889e-03, 1.98412698412698412698e-04,
+                            2.48015873015873015873e-05, 2.75573192239858906526e-06,
+                            2.75573192239858906526e-07, 2.50521083854417187751e-08,
+                            2.08767569878680989792e-09};
+  return ldexp(estrin<13>(c, r), ni);
+}
 // exp_ with a degree-11 polynomial: same reduction, one FMA fewer
 __device__ __forceinline__ double exp11_(double x) {
   x = fmax(x, -746.0);
@@ -480,7 +523,7 @@ __device__ __forceinline__ R bin_tail(R iL, R cx, R yi, R isu, R th1, R th2, A (
   acc[3] += (A)w;
   return w * iL;                                                 // dlp/ddL / (th2 th3) * sigma^2
 }
-template <class R, class A, int NA>
+template <class R, class A, int NA, bool LAT = false>
 __device__ __forceinline__ R bin_core(R dL, R cx, R yi, R isu, R th1, R th2, R th3, A (&acc)[NA],
                                       R& umin) {
   const R u = R(1) + dL;
@@ -488,7 +531,9 @@ __device__ __forceinline__ R bin_core(R dL, R cx, R yi, R isu, R th1, R th2, R t
   const R L = th3 * u;                                           // decay length theta3*(1+dL)
   const R iL = rcp_<R>(L);
   const R ciL = cx * iL;                                         // c x / L
-  const R e = exp_<R>(-ciL);                                     // exp(-c x / L)
+  R e;                                                           // exp(-c x / L)
+  if constexpr (LAT && sizeof(R) == 8) e = exp_lat(-ciL);
+  else e = exp_<R>(-ciL);
   const R m = fma(th2, e, th1);                                  // ui.R:88
   const R d = fma(-m, isu, yi);                                  // (y-m)/uy
   const R a = d * isu;                                           // dlp/dm * sigma^2
@@ -520,13 +565,18 @@ __device__ __forceinline__ void bin_poly(R cx, R y, R isu, R t, R av, R th1, R t
 
 // MODE_POLY on a uniform grid: the forward half of bin_poly; returns w = h a,
 // the bin's weight in the moments (accumulated per lane by moments_geo).
-template <class R, int NNP, class A>
+template <class R, int NNP, class A, bool LAT = false>
 __device__ __forceinline__ R bin_poly_fwd(R cx, R y, R isu, R t, R av, R th1, R th2, R th3,
                                           const R (&cf)[NNP], A (&acc)[4 + NNP], R& umin) {
-  R P = cf[NNP - 1];
+  R P;
+  if constexpr (LAT && sizeof(R) == 8) {
+    P = estrin<NNP>(cf, t);
+  } else {
+    P = cf[NNP - 1];
 #pragma unroll
-  for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
-  return bin_core<R, A, 4 + NNP>(av * P, cx, y, isu, th1, th2, th3, acc, umin) * av;
+    for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
+  }
+  return bin_core<R, A, 4 + NNP, LAT>(av * P, cx, y, isu, th1, th2, th3, acc, umin) * av;
 }
 
 // Two bins of bin_poly_fwd sharing one reciprocal: 1/L0 = L1 / (L0 L1), 1/L1 = L0 / (L0 L1)
@@ -748,7 +798,7 @@ struct Lds {
 
 // The likelihood sweep of chains [cb, ce) of the tile (gradient waves only).
 // PART[c][wave][0 .. 4+NNP) receives this wave's partial sums of chain c.
-template <class R, int BPT, int NNP, int MODE>
+template <class R, int BPT, int NNP, int MODE, bool LATOK = true>
 __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                               const AS_LDS double* mpall, AS_LDS double* part, const int* done,
                               int cb, int ce,
@@ -812,10 +862,12 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                                           bins.isu[b + 1], bins.row[b + 1][0], bins.row[b + 1][1],
                                           th1, th2, th3, cf, acc, umin, w[b], w[b + 1]);
         } else {
+          constexpr bool LAT = FITOCT_LAT_SWEEP && LATOK && BPT <= 2;   // latency-bound sweeps
 #pragma unroll
           for (int b = 0; b < BPT; ++b)
-            w[b] = bin_poly_fwd<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
-                                                bins.row[b][1], th1, th2, th3, cf, acc, umin);
+            w[b] = bin_poly_fwd<R, NNP, double, LAT>(bins.cx[b], bins.y[b], bins.isu[b],
+                                                     bins.row[b][0], bins.row[b][1], th1, th2,
+                                                     th3, cf, acc, umin);
         }
         moments_geo<BPT, NNP>(P, bins.row[0][0], w, acc);
       } else {
@@ -2549,8 +2601,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         atomicMax((unsigned long long*)&start_max[c], t);
       }
       if (P.prior_PD == 0)
-        gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1, tid,
-                                         lane, wave);
+        gradient_pass<R, BPT, NNP, MODE, !SPEC>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1,
+                                                tid, lane, wave);
       wave_fence();   // this wave's PART writes are complete
       if (wstamp) t_wbusy += (long long)__builtin_amdgcn_s_memtime() - s0w;
       if (lane == 0) {
