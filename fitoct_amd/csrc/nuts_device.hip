@@ -2426,6 +2426,15 @@ constexpr int RINGN = 16;                 // hand-off ring: >= 2 * GMAX entries
 #ifndef FITOCT_NUTS_WAIT_PRIO
 #define FITOCT_NUTS_WAIT_PRIO 0
 #endif
+// one-chain tiles with deep speculation (A/B knobs, -1 = the NUTS priority): the chain
+// wave's priority while it computes the next prior part during the sweep, and the helper
+// wave's -- each shares its SIMD with a gradient wave of that sweep
+#ifndef FITOCT_DEEP_PRIOR_PRIO
+#define FITOCT_DEEP_PRIOR_PRIO -1
+#endif
+#ifndef FITOCT_HELPER_PRIO
+#define FITOCT_HELPER_PRIO -1
+#endif
 
 // Migration receiver: post NUTS slot c of this tile as free and wait until a
 // crowded tile hands a chain over (returns its chain index, image loaded into
@@ -2627,6 +2636,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     const int c = wave - NGW;
     const bool mig = MIG && P.mig != nullptr;
     if (helped && c == 1) {   // the helper wave of slot 0's chain
+      if (FITOCT_HELPER_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_HELPER_PRIO);
       using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
       Ch ch(P, L, 0, c0, lane, nct);
       int seen = 0;
@@ -2685,7 +2695,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         for (;;) {
           FITOCT_MARK(nuts_loop);
         const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
+        const bool lowp = FITOCT_DEEP_PRIOR_PRIO >= 0 && a == Ch::A_PRIOR && ch.deep;
+        if (lowp) __builtin_amdgcn_s_setprio(FITOCT_DEEP_PRIOR_PRIO);
         const int y = ch.run(a);
+        if (lowp) __builtin_amdgcn_s_setprio(3);
         if (spec && y == Ch::A_SPEC_STAGED) {   // enqueue the speculated position, hand its prior part over
           if (++steps > P.max_steps) {
             ch.Sp->status = ERR_TIMEOUT;
