@@ -112,6 +112,13 @@ struct KParams {
   double* s2_out;           // [points]
   // appended (ABI 5), so the offsets of every field above are those of round 3
   double theta_rate;        // mono-exp, theta_prior = 1: theta_k ~ exponential(theta_rate)
+  // ---- two-ended trajectories (tiles of one chain with deep speculation; 0: off) ----
+  // two producer waves leapfrog the trajectory's backward and forward ends from the
+  // transition's start at once, each into a ring of leaf records; the helper wave books the
+  // leaves in Stan's tree order (nuts_device.hip, "Two-ended trajectories")
+  int bidi;                 // 1: on (the tile's LDS then carves 3 chain areas)
+  int bidi_rb;              // leaf records per ring
+  double* bidi_buf;         // [chains][2][bidi_rb][3 * vlen + 8]
 };
 
 }  // namespace fitoct

@@ -155,6 +155,16 @@ struct ChainScalars {
 };
 static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
 
+// two-ended trajectories (P.bidi): the tile's hand-off words in LDS.  BD_GEN: the transition
+// (1..BD_GEN_MASK, -1: the chain has finished); BD_PROD + s: stream s's published leaves as
+// (gen << 16) | count; BD_CONS + s: leaves of stream s the helper has booked; BD_END: the
+// transition whose tree the helper has ended; BD_EXIT: producers that have left
+enum BdWord : int { BD_GEN = 0, BD_PROD = 1, BD_CONS = 3, BD_END = 5, BD_EXIT = 6, BD_N = 8 };
+constexpr int BD_GEN_MASK = (1 << 15) - 1;
+#ifndef FITOCT_BIDI_LOOK
+#define FITOCT_BIDI_LOOK 1   // a producer runs at most this many doublings past the booked one
+#endif
+
 constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded, never hang a box
 
 __device__ __forceinline__ void wave_fence() {
@@ -798,7 +808,7 @@ struct Lds {
 
 // The likelihood sweep of chains [cb, ce) of the tile (gradient waves only).
 // PART[c][wave][0 .. 4+NNP) receives this wave's partial sums of chain c.
-template <class R, int BPT, int NNP, int MODE, bool LATOK = true>
+template <class R, int BPT, int NNP, int MODE>
 __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                               const AS_LDS double* mpall, AS_LDS double* part, const int* done,
                               int cb, int ce,
@@ -862,7 +872,7 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                                           bins.isu[b + 1], bins.row[b + 1][0], bins.row[b + 1][1],
                                           th1, th2, th3, cf, acc, umin, w[b], w[b + 1]);
         } else {
-          constexpr bool LAT = FITOCT_LAT_SWEEP && LATOK && BPT <= 2;   // latency-bound sweeps
+          constexpr bool LAT = FITOCT_LAT_SWEEP && BPT <= 2;   // latency-bound short sweeps
 #pragma unroll
           for (int b = 0; b < BPT; ++b)
             w[b] = bin_poly_fwd<R, NNP, double, LAT>(bins.cx[b], bins.y[b], bins.isu[b],
@@ -983,6 +993,12 @@ struct Chain {
   volatile AS_LDS int* book_done = nullptr;
   volatile AS_LDS int* book_res = nullptr;
   int book_want = 0;
+  // two-ended trajectories (P.bidi, deep tiles): the producer waves' chain areas (slots 1, 2:
+  // backward, forward) and the tile's hand-off words BD_*
+  bool bidi = false;
+  AS_LDS double* pvb[2] = {nullptr, nullptr};
+  AS_LDS ChainScalars* psp[2] = {nullptr, nullptr};
+  volatile AS_LDS int* bd = nullptr;
   RngKey key;
 
   __device__ Chain(KPc& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
@@ -994,6 +1010,13 @@ struct Chain {
     helped = SPEC && !MIG && nct_ == 1;
     deep = FITOCT_DEEP_SPEC && helped;
     HX = L.hx();
+    bidi = deep && P_.bidi != 0;
+    if (bidi) {
+      pvb[0] = L.vecs(1);
+      pvb[1] = L.vecs(2);
+      psp[0] = &L.cs(1);
+      psp[1] = &L.cs(2);
+    }
     key = make_key(Pr().seed, (uint32_t)gid);
     if constexpr (KROW) {
       const int r = lane < NNP ? lane : 0;
@@ -1340,7 +1363,10 @@ struct Chain {
     // kernel to enqueue and hand to the helper wave, A_SPEC_BOOK then does the leaf's
     // bookkeeping and yields A_SPEC_WAIT (wait for the sweep and the helper, then A_GRAD)
     // or A_SPEC_DISCARD (the trajectory ended: drain both, then A_END_TREE)
-    A_SPEC_STAGED, A_SPEC_BOOK, A_SPEC_WAIT, A_SPEC_DISCARD
+    A_SPEC_STAGED, A_SPEC_BOOK, A_SPEC_WAIT, A_SPEC_DISCARD,
+    // two-ended trajectories: the producers and the helper grow and book the whole tree;
+    // the chain's wave waits for its end, then A_END_TREE
+    A_BIDI_TREE
   };
   enum LeafBook : int { LB_MID = 0, LB_NEXT = 1, LB_END = 2 };
 
@@ -1659,6 +1685,7 @@ struct Chain {
 
   __device__ int act_begin_subtree() {
     FITOCT_MARK(act_begin_subtree);
+    if (bidi) return bidi_begin();   // reached at depth 0 only: the helper books from there on
     const int d = uni(Sp->depth);
     const double u = uniform(key, (uint32_t)uni(Sp->t), TAG_DIR, (uint32_t)d, 0u);
     const int dir = (u > 0.5) ? 1 : 0;
@@ -1814,9 +1841,6 @@ struct Chain {
   // act_spec_book advances them -- the chain's wave reads them only after waiting for this
   // booking.  Same operations on the same values as the plain path: same draws.
   __device__ int deep_book() {
-    const int d = uni(Sp->depth), j = uni(Sp->leaf);
-    const uint32_t t = (uint32_t)uni(Sp->t);
-    tree_uniforms(d, j, t);
     V q, pe, g;
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
@@ -1824,7 +1848,13 @@ struct Chain {
       pe.a[s] = HX[VLEN + idx(s)];
       g.a[s] = HX[2 * VLEN + idx(s)];
     }
-    const double lp = HX[3 * VLEN], s2 = HX[3 * VLEN + 1];
+    return book_leaf(q, pe, g, HX[3 * VLEN], HX[3 * VLEN + 1]);
+  }
+  // ... of a leaf given by value (deep_book: from HX; bidi_book: from a producer's ring)
+  __device__ int book_leaf(const V& q, const V& pe, const V& g, const double lp, const double s2) {
+    const int d = uni(Sp->depth), j = uni(Sp->leaf);
+    const uint32_t t = (uint32_t)uni(Sp->t);
+    tree_uniforms(d, j, t);
     const V minv = ld(V_MINV);
     double h = -lp + kin(pe, minv);
     if (isnan(h)) h = INFINITY;
@@ -1861,6 +1891,73 @@ struct Chain {
     const int r = uni(*book_res);
     book_want = 0;
     return r;
+  }
+
+  // ---------------- two-ended trajectories (P.bidi; tiles of one chain) ----------------
+  // Stan's trajectory grows by doublings in directions drawn per depth (TAG_DIR), and the
+  // leaves of all doublings in one direction form one unbroken leapfrog chain from the
+  // transition's start (a new subtree starts from the end the previous one in that direction
+  // left).  So the backward and the forward chain can be integrated at once, by two producer
+  // waves (slots 1 and 2) sharing the tile's gradient waves, while the helper books the leaves
+  // in tree order from their rings -- the same leaves, momenta, gradients and bookkeeping as the
+  // one-ended path, so the same draws; the period per transition falls from the sum of the two
+  // chains' leaves towards the longer one.  The chain's wave only starts and ends transitions.
+  __device__ AS_GLB double* brec(int s, int n) const {
+    constexpr int REC = 3 * VLEN + 8;
+    const int rb = Pr().bidi_rb;
+    return (AS_GLB double*)Pr().bidi_buf + (((size_t)lc * 2 + s) * rb + (size_t)(n % rb)) * REC;
+  }
+  // the chain's wave, at depth 0 of a transition: act_begin_subtree's bookkeeping, the start
+  // to both producers' slots, then the transition's number (BD_GEN) releases them
+  __device__ int bidi_begin() {
+    const uint32_t t = (uint32_t)uni(Sp->t);
+    const int dir = (uniform(key, t, TAG_DIR, 0u, 0u) > 0.5) ? 1 : 0;
+    Sp->dir = dir;
+    const V q = ld(V_E0_Q), p = ld(V_E0_P), g = ld(V_E0_G), minv = ld(V_MINV);   // E0 = E1 = start
+    st(V_PNEAR, p);
+    Sp->leaf = 0;
+    if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;
+    Sp->lf_e = dir ? Sp->eps_used : -Sp->eps_used;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#pragma unroll
+      for (int s = 0; s < PPL; ++s) {
+        pvb[k][V_E0_Q * VLEN + idx(s)] = q.a[s];
+        pvb[k][V_E0_P * VLEN + idx(s)] = p.a[s];
+        pvb[k][V_E0_G * VLEN + idx(s)] = g.a[s];
+        pvb[k][V_MINV * VLEN + idx(s)] = minv.a[s];
+      }
+      if (lane == 0) {
+        psp[k]->eps_used = Sp->eps_used;
+        psp[k]->t = (int)t;
+        psp[k]->end_lp[0] = Sp->end_lp[0];
+        psp[k]->end_s2[0] = Sp->end_s2[0];
+      }
+    }
+    if (lane == 0) {
+      bd[BD_CONS] = 0;
+      bd[BD_CONS + 1] = 0;
+    }
+    wave_fence();   // every store above lands before the transition's number
+    if (lane == 0) bd[BD_GEN] = (bd[BD_GEN] & BD_GEN_MASK) % BD_GEN_MASK + 1;
+    return A_BIDI_TREE;
+  }
+  // the helper: book leaf n of stream s (published: its record is in L2).  The record is read
+  // past the CU's vector L1 (device-coherent loads): the ring's slots are rewritten every
+  // transition, and an L1 line of the last read of a slot would be stale
+  static __device__ __forceinline__ double l2_load(const AS_GLB double* p) {
+    return __hip_atomic_load((double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ int bidi_book(int s, int n) {
+    const AS_GLB double* r = brec(s, n);
+    V q, pe, g;
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      q.a[k] = l2_load(r + idx(k));
+      pe.a[k] = l2_load(r + VLEN + idx(k));
+      g.a[k] = l2_load(r + 2 * VLEN + idx(k));
+    }
+    return book_leaf(q, pe, g, l2_load(r + 3 * VLEN), l2_load(r + 3 * VLEN + 1));
   }
 
   // run by the helper wave for the leaf being booked: its Hamiltonian and multinomial
@@ -2361,7 +2458,9 @@ struct Chain {
         pp = (KPc*)(((uint64_t)hi << 32) | lo);
       }
       asm volatile("" : "+s"(a), "+s"(pp));
-      if (a == A_YIELD || a == A_SPEC_STAGED || a == A_SPEC_WAIT || a == A_SPEC_DISCARD) break;
+      if (a == A_YIELD || a == A_SPEC_STAGED || a == A_SPEC_WAIT || a == A_SPEC_DISCARD ||
+          a == A_BIDI_TREE)
+        break;
       const bool prof = kProfile && Pr().stamps != nullptr;
       const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
       const int a0 = a;
@@ -2509,11 +2608,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   }
   KPc& P = *((KPc*)Pg + pidx);   // device-resident parameter block: uniform s_load reads
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds<PPL> L{(AS_LDS char*)smem, P.G, Lds<PPL>::chain_bytes(P.max_depth)};
+  // two-ended trajectories carve two more chain areas (the producers' slots 1, 2)
+  const Lds<PPL> L{(AS_LDS char*)smem, P.bidi ? 3 : P.G, Lds<PPL>::chain_bytes(P.max_depth)};
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nct = min(P.G, P.chains - c0);
   __shared__ unsigned long long ring[RINGN];
+  __shared__ int bd[BD_N];   // two-ended trajectories' hand-off words (BdWord)
   __shared__ int q_reserve, n_active, grad_cnt[GMAX];
   __shared__ long long done_t[GMAX];   // profiling build: when the 8th wave finished chain c
   __shared__ long long start_min[GMAX], start_max[GMAX];
@@ -2523,6 +2624,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   __shared__ int help_req, help_done, help_wdone, help_arg[3], help_res;
   const bool spec = SPEC;
   const bool helped = SPEC && !MIG && nct == 1;   // a spare NUTS wave helps the tile's one chain
+  const bool bidi = helped && FITOCT_DEEP_SPEC && P.bidi != 0;   // ... and two producer waves
   __shared__ int live_chains;   // chains the tile hosts (speculation policy, Chain::live)
 
   load_kinv<PPL, NNP>(P, L, tid);
@@ -2542,6 +2644,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     start_max[tid] = 0;
   }
   if (tid < RINGN) ring[tid] = ~0ULL;
+  if (tid < BD_N) bd[tid] = 0;
   if (MIG && P.mig != nullptr) {   // every slot of the tile may host migrants: all NUTS waves live
     if (tid == 0) {
       const MigView M(P.mig, P.mig_tiles);
@@ -2610,8 +2713,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         atomicMax((unsigned long long*)&start_max[c], t);
       }
       if (P.prior_PD == 0)
-        gradient_pass<R, BPT, NNP, MODE, !SPEC>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1,
-                                                tid, lane, wave);
+        gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1, tid,
+                                         lane, wave);
       wave_fence();   // this wave's PART writes are complete
       if (wstamp) t_wbusy += (long long)__builtin_amdgcn_s_memtime() - s0w;
       if (lane == 0) {
@@ -2635,7 +2738,183 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     }
     const int c = wave - NGW;
     const bool mig = MIG && P.mig != nullptr;
-    if (helped && c == 1) {   // the helper wave of slot 0's chain
+    if (bidi && c == 1) {   // two-ended trajectories: book every leaf in tree order
+      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
+      Ch ch(P, L, 0, c0, lane, nct);
+      ch.bd = (volatile AS_LDS int*)bd;
+      int seen = 0;
+      for (;;) {
+        int g;
+        long long spins = 0;
+        unsigned long long t_idle = 0;
+        bool quit = false;
+        while ((g = lds_load(&bd[BD_GEN])) == seen) {   // the next transition, or the end
+          if (++spins > SPIN_LIMIT) {   // hang guard in real time (init, step-size searches)
+            if (spins == SPIN_LIMIT + 1) t_idle = __builtin_amdgcn_s_memrealtime();
+            if (__builtin_amdgcn_s_memrealtime() - t_idle > MIG_WAIT_TICKS) {
+              quit = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(32);
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (quit || g < 0) break;
+        seen = g;
+        wave_fence();   // the transition's start state is read after its number
+        int cons0 = 0, cons1 = 0;
+        for (;;) {
+          const int s = ch.uni(ch.Sp->dir);   // the subtree being booked grows this end
+          const int n = s ? cons1 : cons0;
+          long long sp = 0;
+          for (;;) {   // leaf n of stream s published for this transition
+            const int w = lds_load(&bd[BD_PROD + s]);
+            if ((w >> 16) == g && (w & 0xFFFF) > n) break;
+            if (++sp > SPIN_LIMIT || lds_load(&bd[BD_GEN]) != g) {   // never, short of a fault
+              sp = SPIN_LIMIT + 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          int r = Ch::LB_END;
+          if (sp > SPIN_LIMIT) {
+            ch.Sp->status = ERR_TIMEOUT;
+          } else {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the record after its count
+            r = ch.bidi_book(s, n);
+            if (s) ++cons1;
+            else ++cons0;
+            wave_fence();
+            if (lane == 0) __atomic_store_n(&bd[BD_CONS + s], n + 1, __ATOMIC_RELAXED);
+          }
+          if (r == Ch::LB_END) {
+            wave_fence();   // the booking's LDS writes land before the end is published
+            if (lane == 0) __atomic_store_n(&bd[BD_END], g, __ATOMIC_RELAXED);
+            break;
+          }
+        }
+      }
+    }
+    if (bidi && c >= 2) {   // two-ended trajectories: producer of the backward (c = 2) / forward end
+      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
+      const int s = c - 2, slot = c - 1;
+      Ch pr(P, L, slot, c0, lane, nct);
+      const AS_LDS ChainScalars& S0 = L.cs(0);   // the booked depth (the helper's)
+      long long epoch = 0;
+      int seen = 0;
+      bool quit = false;
+      while (!quit) {
+        int g;
+        {
+          long long spins = 0;
+          unsigned long long t_idle = 0;
+          while ((g = lds_load(&bd[BD_GEN])) == seen) {
+            if (++spins > SPIN_LIMIT) {
+              if (spins == SPIN_LIMIT + 1) t_idle = __builtin_amdgcn_s_memrealtime();
+              if (__builtin_amdgcn_s_memrealtime() - t_idle > MIG_WAIT_TICKS) {
+                quit = true;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(32);
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        if (quit || g < 0) break;
+        seen = g;
+        wave_fence();
+        Vd<PPL> q = pr.ld(V_E0_Q), p = pr.ld(V_E0_P), gr = pr.ld(V_E0_G);
+        const Vd<PPL> minv = pr.ld(V_MINV);
+        const double eps = pr.Sp->eps_used;
+        const uint32_t t = (uint32_t)pr.uni(pr.Sp->t);
+        // lane k: this end's leaves through doubling k (directions: act_begin_subtree's draws)
+        int cum = 0;
+        if (lane < P.max_depth) {
+          const int dk = (uniform(pr.key, t, TAG_DIR, (uint32_t)lane, 0u) > 0.5) ? 1 : 0;
+          cum = (dk == s) ? (1 << lane) : 0;
+        }
+#pragma unroll
+        for (int o = 1; o < MAXDEPTH; o <<= 1) {
+          const int v = __shfl_up(cum, o);
+          if (lane >= o) cum += v;
+        }
+        wave_fence();
+        if (lds_load(&bd[BD_GEN]) != g) continue;   // the start was rewritten while read
+        const double e = s ? eps : -eps;
+        int n = 0;
+        for (;;) {
+          bool go = false;
+          long long spins = 0;
+          for (;;) {   // within FITOCT_BIDI_LOOK doublings of the booked one, and the ring
+            if (lds_load(&bd[BD_GEN]) != g) break;
+            const int dl = min(pr.uni(*(volatile const AS_LDS int*)&S0.depth) + FITOCT_BIDI_LOOK,
+                               P.max_depth - 1);
+            const int lim = pr.uni(__shfl(cum, dl));
+            const int cons = lds_load(&bd[BD_CONS + s]);
+            if (n < lim && n - cons < P.bidi_rb) {
+              go = true;
+              break;
+            }
+            if (++spins > SPIN_LIMIT) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (!go) break;   // the tree ended (next transition or the end)
+          // expl_leapfrog from the last leaf of this end: begin_update_p, update_q
+          Vd<PPL> p1, q1;
+#pragma unroll
+          for (int k = 0; k < PPL; ++k) {
+            p1.a[k] = fma(0.5 * e, gr.a[k], p.a[k]);
+            q1.a[k] = fma(e, minv.a[k] * p1.a[k], q.a[k]);
+          }
+          pr.write_mp(q1);
+          if (lane == 0) {
+            const unsigned rs = (unsigned)atomicAdd(&q_reserve, 1);
+            __atomic_store_n(&ring[rs % RINGN], ((unsigned long long)rs << 32) | (unsigned)slot,
+                             __ATOMIC_RELAXED);
+          }
+          ++epoch;
+          pr.prior_part();   // overlaps the sweep
+          long long ws = 0;
+          while (lds_load(&grad_cnt[slot]) < (int)(NGW * epoch)) {
+            if (++ws > SPIN_LIMIT) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (ws > SPIN_LIMIT) {
+            quit = true;
+            break;
+          }
+          wave_fence();
+          Vd<PPL> gn;
+          double s2;
+          const double lp = pr.finish_grad(gn, s2);
+          Vd<PPL> pe;
+#pragma unroll
+          for (int k = 0; k < PPL; ++k) pe.a[k] = fma(0.5 * e, gn.a[k], p1.a[k]);   // end_update_p
+          if (lds_load(&bd[BD_GEN]) != g) break;   // the tree has ended: the leaf is not needed
+          AS_GLB double* r = pr.brec(s, n);
+#pragma unroll
+          for (int k = 0; k < PPL; ++k) {
+            r[pr.idx(k)] = q1.a[k];
+            r[Ch::VLEN + pr.idx(k)] = pe.a[k];
+            r[2 * Ch::VLEN + pr.idx(k)] = gn.a[k];
+          }
+          if (lane == 0) {
+            r[3 * Ch::VLEN] = lp;
+            r[3 * Ch::VLEN + 1] = s2;
+          }
+          // the record's stores complete (in L2) before its count is published
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) __atomic_store_n(&bd[BD_PROD + s], (g << 16) | (n + 1), __ATOMIC_RELAXED);
+          q = q1;
+          p = pe;
+          gr = gn;
+          ++n;
+        }
+      }
+      wave_fence();
+      if (lane == 0) atomicAdd(&bd[BD_EXIT], 1);
+    }
+    if (helped && !bidi && c == 1) {   // the helper wave of slot 0's chain
       if (FITOCT_HELPER_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_HELPER_PRIO);
       using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
       Ch ch(P, L, 0, c0, lane, nct);
@@ -2688,6 +2967,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
        if (lc >= 0) {
         Ch ch(P, L, c, lc, lane, nct);
         ch.live = (const AS_LDS int*)&live_chains;
+        ch.bd = (volatile AS_LDS int*)bd;
         long long steps = 0;
         bool in_sweep = false;   // the last run() was A_PRIOR, overlapping the chain's sweep
         // ONE call site of the action machine (it is inlined once, not per caller)
@@ -2699,6 +2979,22 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if (lowp) __builtin_amdgcn_s_setprio(FITOCT_DEEP_PRIOR_PRIO);
         const int y = ch.run(a);
         if (lowp) __builtin_amdgcn_s_setprio(3);
+        if (spec && y == Ch::A_BIDI_TREE) {   // the producers and the helper grow the tree
+          const int g = lds_load(&bd[BD_GEN]);
+          long long spins = 0;
+          while (lds_load(&bd[BD_END]) != g) {
+            if (++spins > SPIN_LIMIT) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          wave_fence();   // the helper's bookkeeping is read after the end
+          if (spins > SPIN_LIMIT || ch.uni(ch.Sp->status) == ERR_TIMEOUT) {
+            ch.Sp->status = ERR_TIMEOUT;
+            a = Ch::A_FINISH;
+          } else {
+            a = Ch::A_END_TREE;
+          }
+          continue;
+        }
         if (spec && y == Ch::A_SPEC_STAGED) {   // enqueue the speculated position, hand its prior part over
           if (++steps > P.max_steps) {
             ch.Sp->status = ERR_TIMEOUT;
@@ -2819,6 +3115,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             atomicAdd(&chains_done_here, 1);
           }
           if (helped && lane == 0) __atomic_store_n(&help_req, -1, __ATOMIC_RELAXED);   // release the helper
+          if (bidi) {   // release the producers and the helper; the producers drain their sweeps
+            if (lane == 0) __atomic_store_n(&bd[BD_GEN], -1, __ATOMIC_RELAXED);
+            long long spins = 0;
+            while (lds_load(&bd[BD_EXIT]) < 2 && ++spins < SPIN_LIMIT) __builtin_amdgcn_s_sleep(1);
+          }
           if (spec && lane == 0) atomicSub(&live_chains, 1);
           break;
         }
@@ -2978,7 +3279,7 @@ template <class R, int BPT, int NNP, int PPL, int MODE>
 static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int tiles,
                            hipStream_t st, const int* tile_map) {
   constexpr int F = FITOCT_FAMILY;
-  const int lds = Lds<PPL>::bytes(P.G, P.max_depth);
+  const int lds = Lds<PPL>::bytes(!logp && P.bidi ? 3 : P.G, P.max_depth);   // bidi: 3 chain areas
   if (logp) {
     auto k = logp_kernel<R, BPT, NNP, PPL, MODE, F>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

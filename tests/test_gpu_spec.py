@@ -141,3 +141,43 @@ def test_headline_tiles_fit_four_chains_at_depth_12():
         with Plan(prob, cfg) as pl:
             assert pl.info["chains_per_tile"] == 4, (depth, pl.info)
             assert pl.info["sampler"] == 3 and pl.info["lds_bytes"] <= 160 * 1024
+
+
+@pytest.mark.parametrize("family,N,depth,rb", [("normal", 512, 10, None), ("normal", 512, 4, "2"),
+                                               ("horseshoe", 2048, 8, "3"), ("lasso", 300, 12, None)])
+def test_two_ended_trajectories_preserve_draws_bitwise(family, N, depth, rb):
+    """Tiles of one chain grow both ends of each trajectory at once (two producer waves,
+    leaf rings in HBM, the helper booking in tree order; nuts_device.hip "Two-ended
+    trajectories"): same draws, step sizes, metrics and leapfrog counts as the one-ended
+    deep-speculation path (FITOCT_NO_BIDI=1), also with rings of 2-3 records (producers
+    throttled by the booking) and with trees cut at max_treedepth 4."""
+    prob = _prob(family, N, 15)
+    cfg = SamplerConfig(chains=24, warmup=80, samples=60, seed=35, max_treedepth=depth)
+    info, a = _run_env(prob, cfg, FITOCT_NO_BIDI=None, FITOCT_BIDI_RB=rb, FITOCT_NO_SPEC=None)
+    info0, b = _run_env(prob, cfg, FITOCT_NO_BIDI="1", FITOCT_BIDI_RB=None, FITOCT_NO_SPEC=None)
+    assert info["chains_per_tile"] == 1 and info["sampler"] == 2
+    assert info["lds_bytes"] > info0["lds_bytes"]   # the producers' two chain areas
+    np.testing.assert_array_equal(a.draws, b.draws)
+    np.testing.assert_array_equal(a.stepsize, b.stepsize)
+    np.testing.assert_array_equal(a.inv_metric, b.inv_metric)
+    assert a.total_leapfrogs == b.total_leapfrogs
+
+
+def test_batch_of_one_chain_tiles_two_ended_bitwise():
+    """A batch whose tiles host one chain each (few files: config 5 spread over 8 GPUs)
+    takes the two-ended path per problem: same draws as without it."""
+    from fitoct_amd import sample_batch
+    probs = [_prob("normal", 481, 15, seed=60 + f) for f in range(5)]
+    cfg = SamplerConfig(chains=4, warmup=40, samples=30, seed=11)
+    old = {k: os.environ.pop(k, None) for k in ("FITOCT_NO_SPEC", "FITOCT_SPEC", "FITOCT_NO_BIDI")}
+    try:
+        a = sample_batch(probs, cfg)
+        os.environ["FITOCT_NO_BIDI"] = "1"
+        b = sample_batch(probs, cfg)
+    finally:
+        for k, v in old.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x.draws, y.draws)
