@@ -449,7 +449,6 @@ void free_plan(fitoct_plan* pl) {
   (void)hipFree(pl->d_data);
   (void)hipFree(pl->d_draws);
   (void)hipFree(pl->d_stack);
-  (void)hipFree(pl->d_bidi);
   (void)hipFree(pl->d_fin);
   (void)hipFree(pl->d_init);
   (void)hipFree(pl->d_status);
@@ -794,24 +793,22 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   }
   // Two-ended trajectories (nuts_device.hip): tiles of one chain with deep speculation grow
   // the trajectory's two ends at once on two spare NUTS waves, each into a ring of leaf
-  // records in HBM; the tile's LDS carves two more chain areas for them.  Same draws bit for
-  // bit.  FITOCT_NO_BIDI=1: off; FITOCT_BIDI_RB=n: records per ring (default 128).
+  // records in the tile's LDS, behind two more chain areas for them.  Same draws bit for bit.
+  // The rings take what LDS is left (at most 128 records each; off below 4).
+  // FITOCT_NO_BIDI=1: off; FITOCT_BIDI_RB=n: at most n records per ring.
   k.bidi = 0;
-  if (k.spec && k.G == 1 && pl->mig_bytes == 0 && getenv("FITOCT_NO_BIDI") == nullptr &&
-      lds_bytes(pl->ppl, 3, k.max_depth) <= 160 * 1024 - 256) {
-    int rb = 128;
-    if (const char* e = getenv("FITOCT_BIDI_RB")) rb = std::max(1, std::min(atoi(e), 1 << 16));
-    const size_t rec = 3 * (size_t)vlen + 8;
-    auto bidi_setup = [&]() -> int {
-      HIP_TRY(hipMalloc(&pl->d_bidi, sizeof(double) * (size_t)C * 2 * rb * rec));
-      return FITOCT_OK;
-    };
-    rc = bidi_setup();
-    if (rc) return rc;
-    k.bidi = 1;
-    k.bidi_rb = rb;
-    k.bidi_buf = pl->d_bidi;
-    pl->lds = lds_bytes(pl->ppl, 3, k.max_depth);
+  if (k.spec && k.G == 1 && pl->mig_bytes == 0 && getenv("FITOCT_NO_BIDI") == nullptr) {
+    const int rec = (3 * D + 2 + 1) / 2 * 2;   // doubles, 16-byte records
+    const int base = lds_bytes(pl->ppl, 3, k.max_depth);
+    const int avail = 160 * 1024 - 256 - 1024 - base;   // 1 KB for the kernel's static LDS
+    int rb = avail > 0 ? std::min(128, avail / (2 * rec * 8)) : 0;
+    if (const char* e = getenv("FITOCT_BIDI_RB")) rb = std::min(rb, std::max(1, atoi(e)));
+    if (rb >= 4 || (getenv("FITOCT_BIDI_RB") && rb >= 1)) {
+      k.bidi = 1;
+      k.bidi_rb = rb;
+      k.bidi_rec = rec;
+      pl->lds = base + 2 * rb * rec * 8;
+    }
   }
   *out = guard.release();
   return FITOCT_OK;

@@ -117,8 +117,8 @@ struct KParams {
   // transition's start at once, each into a ring of leaf records; the helper wave books the
   // leaves in Stan's tree order (nuts_device.hip, "Two-ended trajectories")
   int bidi;                 // 1: on (the tile's LDS then carves 3 chain areas)
-  int bidi_rb;              // leaf records per ring
-  double* bidi_buf;         // [chains][2][bidi_rb][3 * vlen + 8]
+  int bidi_rb;              // leaf records per ring (two rings in LDS after the chain areas)
+  int bidi_rec;             // doubles per record: q, end-updated p, g (D each), lp, sum r^2
 };
 
 }  // namespace fitoct

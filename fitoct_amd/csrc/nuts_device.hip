@@ -1902,10 +1902,11 @@ struct Chain {
   // in tree order from their rings -- the same leaves, momenta, gradients and bookkeeping as the
   // one-ended path, so the same draws; the period per transition falls from the sum of the two
   // chains' leaves towards the longer one.  The chain's wave only starts and ends transitions.
-  __device__ AS_GLB double* brec(int s, int n) const {
-    constexpr int REC = 3 * VLEN + 8;
+  // record n of stream s: [q (D) | end-updated p (D) | g (D) | lp | sum r^2] in the LDS ring
+  // behind the three chain areas (where HX would be)
+  __device__ AS_LDS double* brec(int s, int n) const {
     const int rb = Pr().bidi_rb;
-    return (AS_GLB double*)Pr().bidi_buf + (((size_t)lc * 2 + s) * rb + (size_t)(n % rb)) * REC;
+    return HX + (s * rb + n % rb) * Pr().bidi_rec;
   }
   // the chain's wave, at depth 0 of a transition: act_begin_subtree's bookkeeping, the start
   // to both producers' slots, then the transition's number (BD_GEN) releases them
@@ -1942,22 +1943,20 @@ struct Chain {
     if (lane == 0) bd[BD_GEN] = (bd[BD_GEN] & BD_GEN_MASK) % BD_GEN_MASK + 1;
     return A_BIDI_TREE;
   }
-  // the helper: book leaf n of stream s (published: its record is in L2).  The record is read
-  // past the CU's vector L1 (device-coherent loads): the ring's slots are rewritten every
-  // transition, and an L1 line of the last read of a slot would be stale
-  static __device__ __forceinline__ double l2_load(const AS_GLB double* p) {
-    return __hip_atomic_load((double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  // the helper: book leaf n of stream s (published: its record is in the ring).  Lanes past D
+  // read 0, the value every padding lane of q, p and g holds
   __device__ int bidi_book(int s, int n) {
-    const AS_GLB double* r = brec(s, n);
+    const AS_LDS double* r = brec(s, n);
+    const int D = Pr().D;
     V q, pe, g;
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
-      q.a[k] = l2_load(r + idx(k));
-      pe.a[k] = l2_load(r + VLEN + idx(k));
-      g.a[k] = l2_load(r + 2 * VLEN + idx(k));
+      const bool in = ok(k);
+      q.a[k] = in ? r[idx(k)] : 0.0;
+      pe.a[k] = in ? r[D + idx(k)] : 0.0;
+      g.a[k] = in ? r[2 * D + idx(k)] : 0.0;
     }
-    return book_leaf(q, pe, g, l2_load(r + 3 * VLEN), l2_load(r + 3 * VLEN + 1));
+    return book_leaf(q, pe, g, r[3 * D], r[3 * D + 1]);
   }
 
   // run by the helper wave for the leaf being booked: its Hamiltonian and multinomial
@@ -2891,19 +2890,21 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
 #pragma unroll
           for (int k = 0; k < PPL; ++k) pe.a[k] = fma(0.5 * e, gn.a[k], p1.a[k]);   // end_update_p
           if (lds_load(&bd[BD_GEN]) != g) break;   // the tree has ended: the leaf is not needed
-          AS_GLB double* r = pr.brec(s, n);
+          AS_LDS double* r = pr.brec(s, n);
+          const int D = P.D;
 #pragma unroll
           for (int k = 0; k < PPL; ++k) {
-            r[pr.idx(k)] = q1.a[k];
-            r[Ch::VLEN + pr.idx(k)] = pe.a[k];
-            r[2 * Ch::VLEN + pr.idx(k)] = gn.a[k];
+            if (pr.ok(k)) {
+              r[pr.idx(k)] = q1.a[k];
+              r[D + pr.idx(k)] = pe.a[k];
+              r[2 * D + pr.idx(k)] = gn.a[k];
+            }
           }
           if (lane == 0) {
-            r[3 * Ch::VLEN] = lp;
-            r[3 * Ch::VLEN + 1] = s2;
+            r[3 * D] = lp;
+            r[3 * D + 1] = s2;
           }
-          // the record's stores complete (in L2) before its count is published
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          wave_fence();   // the record lands before its count
           if (lane == 0) __atomic_store_n(&bd[BD_PROD + s], (g << 16) | (n + 1), __ATOMIC_RELAXED);
           q = q1;
           p = pe;
@@ -3279,7 +3280,9 @@ template <class R, int BPT, int NNP, int PPL, int MODE>
 static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int tiles,
                            hipStream_t st, const int* tile_map) {
   constexpr int F = FITOCT_FAMILY;
-  const int lds = Lds<PPL>::bytes(!logp && P.bidi ? 3 : P.G, P.max_depth);   // bidi: 3 chain areas
+  // two-ended trajectories: 3 chain areas, then the two leaf rings
+  const int lds = (!logp && P.bidi) ? Lds<PPL>::bytes(3, P.max_depth) + 2 * P.bidi_rb * P.bidi_rec * 8
+                                    : Lds<PPL>::bytes(P.G, P.max_depth);
   if (logp) {
     auto k = logp_kernel<R, BPT, NNP, PPL, MODE, F>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

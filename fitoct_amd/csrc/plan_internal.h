@@ -24,7 +24,6 @@ struct fitoct_plan {
   void* d_data = nullptr;     // cx | y | isu | B  (type R)
   double* d_draws = nullptr;  // internal draws buffer (lazily allocated)
   double* d_stack = nullptr;
-  double* d_bidi = nullptr;   // two-ended trajectories' leaf rings (KParams::bidi_buf)
   double* d_fin = nullptr;    // eps[C] | minv[C*D] | q[C*D]
   double* d_init = nullptr;   // warm restart (fitoct_plan_set_init): eps[C] | minv[C*D] | q[C*D]
   int* d_status = nullptr;
