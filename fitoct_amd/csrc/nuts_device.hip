@@ -162,7 +162,7 @@ static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
 enum BdWord : int { BD_GEN = 0, BD_PROD = 1, BD_CONS = 3, BD_END = 5, BD_EXIT = 6, BD_N = 8 };
 constexpr int BD_GEN_MASK = (1 << 15) - 1;
 #ifndef FITOCT_BIDI_LOOK
-#define FITOCT_BIDI_LOOK 1   // a producer runs at most this many doublings past the booked one
+#define FITOCT_BIDI_LOOK 3   // a producer runs at most this many doublings past the booked one
 #endif
 
 constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded, never hang a box
