@@ -41,6 +41,7 @@ inline hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams&
   }
 }
 int lds_bytes(int ppl, int G, int max_depth);
+int lvl_doubles(int ppl, int max_depth);
 int mig_img_words(int ppl);
 }  // namespace fitoct
 
@@ -794,20 +795,22 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   // Two-ended trajectories (nuts_device.hip): tiles of one chain with deep speculation grow
   // the trajectory's two ends at once on two spare NUTS waves, each into a ring of leaf
   // records in the tile's LDS, behind two more chain areas for them.  Same draws bit for bit.
-  // The rings take what LDS is left (at most 128 records each; off below 4).
-  // FITOCT_NO_BIDI=1: off; FITOCT_BIDI_RB=n: at most n records per ring.
+  // Each ring fills its producer's unused tree-level area, then takes what LDS is left (at most
+  // 256 records each; off below 4).  FITOCT_NO_BIDI=1: off; FITOCT_BIDI_RB=n: at most n records.
   k.bidi = 0;
   if (k.spec && k.G == 1 && pl->mig_bytes == 0 && getenv("FITOCT_NO_BIDI") == nullptr) {
     const int rec = (3 * D + 2 + 1) / 2 * 2;   // doubles, 16-byte records
     const int base = lds_bytes(pl->ppl, 3, k.max_depth);
     const int avail = 160 * 1024 - 256 - 1024 - base;   // 1 KB for the kernel's static LDS
-    int rb = avail > 0 ? std::min(128, avail / (2 * rec * 8)) : 0;
+    const int ra = lvl_doubles(pl->ppl, k.max_depth) / rec;
+    int rb = std::min(256, ra + (avail > 0 ? avail / (2 * rec * 8) : 0));
     if (const char* e = getenv("FITOCT_BIDI_RB")) rb = std::min(rb, std::max(1, atoi(e)));
     if (rb >= 4 || (getenv("FITOCT_BIDI_RB") && rb >= 1)) {
       k.bidi = 1;
       k.bidi_rb = rb;
+      k.bidi_rba = std::min(ra, rb);
       k.bidi_rec = rec;
-      pl->lds = base + 2 * rb * rec * 8;
+      pl->lds = base + 2 * (rb - k.bidi_rba) * rec * 8;
     }
   }
   *out = guard.release();

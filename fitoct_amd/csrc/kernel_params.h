@@ -119,6 +119,8 @@ struct KParams {
   int bidi;                 // 1: on (the tile's LDS then carves 3 chain areas)
   int bidi_rb;              // leaf records per ring (two rings in LDS after the chain areas)
   int bidi_rec;             // doubles per record: q, end-updated p, g (D each), lp, sum r^2
+  int bidi_rba;             // records of each ring in its producer's (unused) tree-level area;
+                            // the other bidi_rb - bidi_rba behind the chain areas
 };
 
 }  // namespace fitoct

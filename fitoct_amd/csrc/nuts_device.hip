@@ -998,6 +998,8 @@ struct Chain {
   bool bidi = false;
   AS_LDS double* pvb[2] = {nullptr, nullptr};
   AS_LDS ChainScalars* psp[2] = {nullptr, nullptr};
+  AS_LDS double* plv0 = nullptr;   // (two scalars: a runtime-indexed member array would put
+  AS_LDS double* plv1 = nullptr;   //  the whole chain object in scratch)
   volatile AS_LDS int* bd = nullptr;
   RngKey key;
 
@@ -1016,6 +1018,8 @@ struct Chain {
       pvb[1] = L.vecs(2);
       psp[0] = &L.cs(1);
       psp[1] = &L.cs(2);
+      plv0 = L.lvls(1);
+      plv1 = L.lvls(2);
     }
     key = make_key(Pr().seed, (uint32_t)gid);
     if constexpr (KROW) {
@@ -1904,9 +1908,12 @@ struct Chain {
   // chains' leaves towards the longer one.  The chain's wave only starts and ends transitions.
   // record n of stream s: [q (D) | end-updated p (D) | g (D) | lp | sum r^2] in the LDS ring
   // behind the three chain areas (where HX would be)
+  // (the first bidi_rba records of ring s sit in producer slot s + 1's tree-level area, which
+  // a producer never uses)
   __device__ AS_LDS double* brec(int s, int n) const {
-    const int rb = Pr().bidi_rb;
-    return HX + (s * rb + n % rb) * Pr().bidi_rec;
+    const int rb = Pr().bidi_rb, ra = Pr().bidi_rba, m = n % rb;
+    return m < ra ? (s ? plv1 : plv0) + m * Pr().bidi_rec
+                  : HX + (s * (rb - ra) + (m - ra)) * Pr().bidi_rec;
   }
   // the chain's wave, at depth 0 of a transition: act_begin_subtree's bookkeeping, the start
   // to both producers' slots, then the transition's number (BD_GEN) releases them
@@ -3267,6 +3274,11 @@ __global__ void __launch_bounds__(TPB, 2) logp_kernel(const KParams* __restrict_
 #define FITOCT_CAT(a, b) FITOCT_CAT2(a, b)
 
 #if FITOCT_FAMILY == 0
+// doubles of a chain area's tree levels and merge-uniform rings (two-ended trajectories keep
+// leaf records there in the producers' areas)
+int lvl_doubles(int ppl, int max_depth) {
+  return max_depth * NLVL * WAVE * ppl + max_depth * WAVE;
+}
 int lds_bytes(int ppl, int G, int max_depth) {
   return ppl == 1 ? Lds<1>::bytes(G, max_depth) : Lds<2>::bytes(G, max_depth);
 }
@@ -3281,7 +3293,8 @@ static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int t
                            hipStream_t st, const int* tile_map) {
   constexpr int F = FITOCT_FAMILY;
   // two-ended trajectories: 3 chain areas, then the two leaf rings
-  const int lds = (!logp && P.bidi) ? Lds<PPL>::bytes(3, P.max_depth) + 2 * P.bidi_rb * P.bidi_rec * 8
+  const int lds = (!logp && P.bidi) ? Lds<PPL>::bytes(3, P.max_depth) +
+                                          2 * (P.bidi_rb - P.bidi_rba) * P.bidi_rec * 8
                                     : Lds<PPL>::bytes(P.G, P.max_depth);
   if (logp) {
     auto k = logp_kernel<R, BPT, NNP, PPL, MODE, F>;
