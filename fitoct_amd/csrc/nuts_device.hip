@@ -2851,6 +2851,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         for (;;) {
           bool go = false;
           long long spins = 0;
+          unsigned long long t_thr = 0;
           for (;;) {   // within FITOCT_BIDI_LOOK doublings of the booked one, and the ring
             if (lds_load(&bd[BD_GEN]) != g) break;
             const int dl = min(pr.uni(*(volatile const AS_LDS int*)&S0.depth) + FITOCT_BIDI_LOOK,
@@ -2861,7 +2862,12 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
               go = true;
               break;
             }
-            if (++spins > SPIN_LIMIT) break;
+            // the other end may grow for long (deep trees, large N): bounded in real time
+            if (++spins > SPIN_LIMIT) {
+              if (spins == SPIN_LIMIT + 1) t_thr = __builtin_amdgcn_s_memrealtime();
+              if (__builtin_amdgcn_s_memrealtime() - t_thr > MIG_WAIT_TICKS) break;
+              __builtin_amdgcn_s_sleep(32);
+            }
             __builtin_amdgcn_s_sleep(1);
           }
           if (!go) break;   // the tree ended (next transition or the end)
@@ -2990,12 +2996,21 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if (spec && y == Ch::A_BIDI_TREE) {   // the producers and the helper grow the tree
           const int g = lds_load(&bd[BD_GEN]);
           long long spins = 0;
-          while (lds_load(&bd[BD_END]) != g) {
-            if (++spins > SPIN_LIMIT) break;
+          unsigned long long t_tree = 0;
+          bool late = false;
+          while (lds_load(&bd[BD_END]) != g) {   // a whole tree: bounded in real time
+            if (++spins > SPIN_LIMIT) {
+              if (spins == SPIN_LIMIT + 1) t_tree = __builtin_amdgcn_s_memrealtime();
+              if (__builtin_amdgcn_s_memrealtime() - t_tree > MIG_WAIT_TICKS) {
+                late = true;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(32);
+            }
             __builtin_amdgcn_s_sleep(1);
           }
           wave_fence();   // the helper's bookkeeping is read after the end
-          if (spins > SPIN_LIMIT || ch.uni(ch.Sp->status) == ERR_TIMEOUT) {
+          if (late || ch.uni(ch.Sp->status) == ERR_TIMEOUT) {
             ch.Sp->status = ERR_TIMEOUT;
             a = Ch::A_FINISH;
           } else {
