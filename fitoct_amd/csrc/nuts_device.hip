@@ -42,6 +42,9 @@
 //     becomes the sample.  Wave reductions are DPP/permlane butterflies.
 //   * workgroups communicate only to hand whole chains between tiles at transition
 //     boundaries (chain migration, the MIG instantiation).
+//   * a tile of one chain (fewer chains than CUs) puts its three spare NUTS waves to work:
+//     two producers leapfrog the trajectory's backward and forward ends at once and a
+//     helper books the leaves in Stan's tree order ("Two-ended trajectories" below).
 //
 // Random numbers are addressable Philox draws (philox.h), identical to the CPU
 // oracle's, so short horizons of GPU and CPU chains coincide draw for draw.
