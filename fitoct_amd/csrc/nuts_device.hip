@@ -164,6 +164,14 @@ static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
 // transition whose tree the helper has ended; BD_EXIT: producers that have left
 enum BdWord : int { BD_GEN = 0, BD_PROD = 1, BD_CONS = 3, BD_END = 5, BD_EXIT = 6, BD_N = 8 };
 constexpr int BD_GEN_MASK = (1 << 15) - 1;
+// the chain's wave while the producers and the helper grow a tree: its priority (-1: the NUTS
+// priority) and poll interval (A/B knobs)
+#ifndef FITOCT_BIDI_IDLE_PRIO
+#define FITOCT_BIDI_IDLE_PRIO -1
+#endif
+#ifndef FITOCT_BIDI_IDLE_SLEEP
+#define FITOCT_BIDI_IDLE_SLEEP 1
+#endif
 #ifndef FITOCT_BIDI_LOOK
 #define FITOCT_BIDI_LOOK 3   // a producer runs at most this many doublings past the booked one
 #endif
@@ -3001,6 +3009,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           long long spins = 0;
           unsigned long long t_tree = 0;
           bool late = false;
+          if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_BIDI_IDLE_PRIO);
           while (lds_load(&bd[BD_END]) != g) {   // a whole tree: bounded in real time
             if (++spins > SPIN_LIMIT) {
               if (spins == SPIN_LIMIT + 1) t_tree = __builtin_amdgcn_s_memrealtime();
@@ -3010,8 +3019,9 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
               }
               __builtin_amdgcn_s_sleep(32);
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(FITOCT_BIDI_IDLE_SLEEP);
           }
+          if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
           wave_fence();   // the helper's bookkeeping is read after the end
           if (late || ch.uni(ch.Sp->status) == ERR_TIMEOUT) {
             ch.Sp->status = ERR_TIMEOUT;
