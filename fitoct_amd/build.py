@@ -28,7 +28,7 @@ SAN_LIB = os.path.join(SAN_DIR, "libfitoct.so")
 SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
 CLANGXX = "/opt/rocm/lib/llvm/bin/clang++"
 # FITOCT_VARIANT=name: an A/B variant library (FITOCT_HIPFLAGS / FITOCT_PROFILE) built to
-# abtest/lib_<name>.so with its own objects, leaving fitoct_amd/libfitoct.so alone; load it
+# ablib/lib_<name>.so with its own objects, leaving fitoct_amd/libfitoct.so alone; load it
 # with FITOCT_LIB_PATH (scripts/ab_libs.sh)
 VARIANT = os.environ.get("FITOCT_VARIANT", "")
 ARCH = os.environ.get("FITOCT_ARCH", "gfx950")
@@ -100,8 +100,8 @@ def build(force: bool = False, verbose: bool = False, sanitize: bool = False) ->
     ``sanitize``, the ASan/UBSan host build ``fitoct_amd/build_san/libfitoct.so``)."""
     objdir, lib = (SAN_DIR, SAN_LIB) if sanitize else (OBJDIR, LIB)
     if VARIANT and not sanitize:
-        objdir = os.path.join(ROOT, "abtest", "obj_" + VARIANT)
-        lib = os.path.join(ROOT, "abtest", f"lib_{VARIANT}.so")
+        objdir = os.path.join(ROOT, "ablib", "obj_" + VARIANT)
+        lib = os.path.join(ROOT, "ablib", f"lib_{VARIANT}.so")
     flags_file = os.path.join(objdir, "flags.txt")
     same_flags = os.path.exists(flags_file) and open(flags_file).read() == _flags()
     if (not force and same_flags and os.path.exists(lib)

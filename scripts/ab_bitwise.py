@@ -1,7 +1,7 @@
-"""Bitwise A/B of variant libraries: every abtest/lib_*.so samples the same short
+"""Bitwise A/B of variant libraries: every ablib/lib_*.so samples the same short
 runs (configs 2, 3, 4 shapes and a batch of config-5 files), and each variant's draws
-are compared bit for bit (SHA-256 of the draw arrays) with abtest/lib_base.so.  Latency-only changes (same
-arithmetic) must print 'identical'.  abtest/env_<name> (KEY=VALUE lines), when present, is added to
+are compared bit for bit (SHA-256 of the draw arrays) with ablib/lib_base.so.  Latency-only changes (same
+arithmetic) must print 'identical'.  ablib/env_<name> (KEY=VALUE lines), when present, is added to
 lib_<name>'s environment (e.g. a copy of a library run with a switch set).
 
     python scripts/ab_bitwise.py            # on the GPU box
@@ -45,11 +45,11 @@ json.dump({k: hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() for 
 
 def main():
     os.makedirs(OUT, exist_ok=True)
-    libs = sorted(glob.glob(os.path.join(ROOT, "abtest", "lib_*.so")))
+    libs = sorted(glob.glob(os.path.join(ROOT, "ablib", "lib_*.so")))
     for lib in libs:
         name = os.path.basename(lib)[4:-3]
         env = dict(os.environ, FITOCT_LIB_PATH=lib)
-        envf = os.path.join(ROOT, "abtest", "env_" + name)
+        envf = os.path.join(ROOT, "ablib", "env_" + name)
         if os.path.exists(envf):
             env.update(line.strip().split("=", 1) for line in open(envf) if "=" in line)
         r = subprocess.run([sys.executable, "-c", RUNNER % ROOT, os.path.join(OUT, name + ".json")],

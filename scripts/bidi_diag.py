@@ -1,5 +1,5 @@
 """Two-ended trajectories vs the one-ended deep path on a few chains: the first iteration
-whose draws differ, with its sampler columns (diagnosis aid for scripts/gpu_r4_bidi.sh)."""
+whose draws differ, with its sampler columns (diagnosis aid for scripts/archive/gpu_r4_bidi.sh)."""
 import os
 import sys
 

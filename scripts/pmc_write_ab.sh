@@ -4,7 +4,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
-for l in ${AB_DIR:-abtest}/lib_*.so; do
+for l in ${AB_DIR:-ablib}/lib_*.so; do
   n=$(basename $l .so)
   d=gpurun_out/pmcw_$n
   FITOCT_LIB_PATH=$PWD/$l timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d -o run -- python3 bench.py --config ${CFG:-3} --steps 1 --warmup 0 --no-cpu --no-hard > $d.log 2>&1 || { echo "$l failed"; tail -5 $d.log; exit 1; }
