@@ -47,6 +47,9 @@ CONFIGS = {
     # extremal, normal prior; files sharded in contiguous blocks over the ranks (strong scaling)
     5: dict(prior="normal", N=481, chains=4, files=256, iters=(100, 100)),
 }
+# the hard-geometry sub-line's step seed: fixed, whatever --steps is, so its R-hat never
+# depends on which seed a step count selects (tests/test_gpu_sampler.py runs it and 1001, 1019)
+HARD_SEED = 1000
 FP64_VALU_PEAK_TF = 78.6          # MI355X FP64 vector peak (vendor spec; 1/2 of FP32 vector)
 HBM_PEAK_GBS = 8000.0
 # PMC traffic summaries (scripts/pmc_traffic.sh [config]), newest round first, matched to
@@ -153,19 +156,17 @@ def convergence(draws, W_saved, cols):
     """Split and rank-normalised R-hat of the post-warmup draws over the parameter
     columns (theta, z / yGP, the scales, sigma, br; the horseshoe's inverse-gamma
     auxiliaries r2_* excluded), with and without the funnel-trapped chains, and the three
-    worst columns by name.  A chain counts as trapped when more than half of its
-    transitions diverge over the run or over either half of it (a chain can fall into the
-    funnel's neck mid-run: seed 1019 at the hard-geometry profile)."""
-    from fitoct_amd.stanfit import rank_rhat, split_rhat_ess
+    worst columns by name.  Trapped: ``fitoct_amd.stanfit.trapped_chains``, the fixed rule
+    (more than half of a chain's transitions diverge over the run or over either half of
+    it); ``stuck_chains_whole_run`` counts by rounds 1-3's whole-run rule."""
+    from fitoct_amd.stanfit import rank_rhat, split_rhat_ess, trapped_chains, trapped_whole_run
     post = draws[:, W_saved:, :]
     par = [j for j, n in enumerate(cols) if j >= 7 and not n.startswith("r2_")]
     rhe = {cols[j]: split_rhat_ess(post[:, :, j]) for j in par}
     rh = {k: v[0] for k, v in rhe.items()}
     ess = {k: v[1] for k, v in rhe.items()}   # rstan n_eff over all chains
     rrh = {cols[j]: rank_rhat(post[:, :, j]) for j in par}   # Vehtari et al. 2021
-    h = post.shape[1] // 2
-    stuck = ((post[:, :, 5].mean(1) > 0.5) | (post[:, :h, 5].mean(1) > 0.5)
-             | (post[:, h:, 5].mean(1) > 0.5))
+    stuck = trapped_chains(post[:, :, 5])
     free = post[~stuck]
     rh_free = {cols[j]: split_rhat_ess(free[:, :, j])[0] for j in par} if stuck.any() else rh
     rrh_free = {cols[j]: rank_rhat(free[:, :, j]) for j in par} if stuck.any() else rrh
@@ -173,6 +174,7 @@ def convergence(draws, W_saved, cols):
     def worst(d):
         return [[k, round(float(v), 5)] for k, v in sorted(d.items(), key=lambda t: -t[1])[:3]]
     return {"rhat_max": round(max(rh.values()), 5), "stuck_chains": int(stuck.sum()),
+            "stuck_chains_whole_run": int(trapped_whole_run(post[:, :, 5]).sum()),
             "rhat_max_excl_stuck": round(max(rh_free.values()), 5),
             "rank_rhat_max": round(max(rrh.values()), 5),
             "rank_rhat_max_excl_stuck": round(max(rrh_free.values()), 5),
@@ -423,11 +425,10 @@ def main():
     bufs.clear()
     if (args.config == 3 and n_units == 1 and not args.no_hard and args.adapt_delta == 0.8
             and args.chains == 0 and (W_it, S_it) == (WARMUP_IT, SAMPLES)):
-        # seed of the last timed step (1000 + steps - 1): not a seed chosen by the builder
         line["hard_geometry"] = hard_geometry(prob, C, local, dev, W_it, S_it, cols,
                                               line.get("cpu_baseline"),
                                               o_means if "cpu_baseline" in line else None,
-                                              seed=1000 + args.steps - 1)
+                                              seed=HARD_SEED)
     if world > 1 and not args.no_device_list:
         # the route R takes (.Call -> fitoct_config.devices), timed on the same node: rank 0
         # alone drives every GPU of the job from one process while the other ranks wait on
@@ -439,7 +440,7 @@ def main():
                 line["device_list"] = device_list_leg(
                     lambda step, devs: Plan(prob, _dl_config(args, C * len(devs), W_it, S_it,
                                                              step, devs)),
-                    _dl_devices(world), C * S_it, dev, f_grad(N_bins, NN))
+                    _dl_devices(world, ndev), C * S_it, dev, f_grad(N_bins, NN))
             except Exception as e:   # noqa: BLE001
                 line["device_list"] = {"error": f"{type(e).__name__}: {e}"}
         dist.barrier(group=hb)
@@ -450,11 +451,20 @@ def main():
         dist.destroy_process_group()
 
 
-def _dl_devices(world):
-    """GPUs of the device-list sub-line: the job's, 0..world-1 (one node, one rank per GPU).
-    FITOCT_BENCH_DEVICE_LIST=0,0 rehearses it with ranks sharing one GPU (gloo backend)."""
+def _dl_devices(world, visible):
+    """GPUs of the device-list sub-line: the job's, one entry per rank (one node, one rank
+    per GPU), each a VISIBLE ordinal: rank r -> r mod visible, so ranks sharing fewer GPUs
+    (a rehearsal on one GPU: 0,0,...) list each card once per rank that uses it.
+    FITOCT_BENCH_DEVICE_LIST=0,1,... overrides; an ordinal outside [0, visible) fails here,
+    before the leg's timed region, with a message."""
     env = os.environ.get("FITOCT_BENCH_DEVICE_LIST", "")
-    return tuple(int(v) for v in env.split(",") if v) or tuple(range(world))
+    devs = tuple(int(v) for v in env.split(",") if v) or tuple(r % max(visible, 1)
+                                                               for r in range(world))
+    bad = [d for d in devs if not 0 <= d < visible]
+    if bad:
+        raise ValueError(f"device list {list(devs)}: ordinals {bad} are not among the "
+                         f"{visible} visible GPU(s)")
+    return devs
 
 
 def _dl_config(args, chains, W_it, S_it, step, devs):
@@ -560,6 +570,7 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it, 
     from fitoct_amd.synth import MODULATIONS, default_prior, synth_decay
 
     conf = CONFIGS[5]
+    ndev = torch.cuda.device_count()
     t0, S0 = default_prior()
     from fitoct_amd.distributed import shard_range
     f_off, f_cnt = shard_range(conf["files"], world, rank)   # contiguous file blocks
@@ -652,6 +663,9 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it, 
                              "torch.distributed" if world > 1 else "single-device")},
         "rhat_max_median_file": round(float(np.median(rh_file)), 4),
         "rhat_max_worst_file": round(float(np.max(rh_file)), 4),
+        # the Shiny app paints R-hat >= 1.1 red (ShinyInterface/server.R:98-100); the C
+        # oracle on the same 256 files gives 27 / 256 (tests/golden/batch_files.npz)
+        "rhat_files_ge_1_1": round(float(np.mean(np.array(rh_file) >= 1.1)), 4),
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TF,
                      "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TF, 4),
                      "traffic": None, "kernel": "nuts_kernel (batched)",
@@ -664,6 +678,12 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it, 
         r["hbm_gbs"] = round(traffic["bytes_per_launch"] / (kernel_ms / 1e3) / 1e9, 2)
         r["hbm_frac"] = round(r["hbm_gbs"] / HBM_PEAK_GBS, 5)
         r["traffic_source"] = traffic["source"]
+    if rank == 0 and n_units == 1 and not args.no_cpu:
+        cb = batch_cpu_baseline(file_problems, conf["files"], C, W_it, S_it, 2000 + args.steps - 1,
+                                outs)
+        line["posterior_mean_relerr_vs_cpu"] = cb.pop("relerr")
+        line["cpu_baseline"] = cb
+        line["gpu_over_cpu"] = round(line["value"] / cb["value"], 1)
     for b in batches:
         b.close()
     bufs.clear()
@@ -681,7 +701,7 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it, 
             try:   # a side measurement: it must not cost the main line
                 every = file_problems(0, conf["files"])
                 line["device_list"] = device_list_leg(
-                    lambda step, devs: batch_for(step, every, 0, devs), _dl_devices(world),
+                    lambda step, devs: batch_for(step, every, 0, devs), _dl_devices(world, ndev),
                     conf["files"] // world * C * S_it, dev, f_grad(conf["N"], NN),
                     is_batch=True)
             except Exception as e:   # noqa: BLE001
@@ -692,6 +712,63 @@ def bench_batch(args, world, rank, local, dev, dist, backend, cdev, W_it, S_it, 
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def batch_cpu_baseline(file_problems, files, C, W, S, seed, gpu_outs, budget_s=12.0):
+    """Config 5's CPU path: the C oracle (one OpenMP thread per chain) on the SAME files,
+    chains (global ids f*C + c), controls and seed as the last timed GPU step, so no
+    scaling is needed: value = files done x C x S / wall.  Bounded: files are run
+    ``share_cpus // C`` at a time from file 0 until ``budget_s`` has passed (the job's
+    CPU share; the rest of the 256 files would run at the same rate).  Posterior means
+    of theta, sigma and br per file against the GPU's same files: median and max of the
+    relative difference over the files run (4 chains x 100 draws per side, so the
+    figure includes both sides' Monte-Carlo error)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from fitoct_amd import SamplerConfig
+    from oracle import nuts_c
+    hw = host_cpu_info()
+    threads = hw["share_cpus"]
+    conc = max(1, threads // C)
+
+    def one(f):
+        prob = file_problems(f, 1)[0]
+        cfg = SamplerConfig(chains=C, chain_offset=f * C, warmup=W, samples=S, seed=seed,
+                            adapt_delta=0.8, max_treedepth=10)
+        o = nuts_c.sample(prob, cfg, nthreads=C)
+        return f, o
+    done = []
+    t = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=conc) as ex:
+        f = 0
+        while f < files and (time.perf_counter() - t < budget_s or not done):
+            done += list(ex.map(one, range(f, min(files, f + conc))))
+            f += conc
+    wall = time.perf_counter() - t
+    cols = file_problems(0, 1)[0].column_names()
+    names = [n for n in cols if n.startswith("theta") or n in ("sigma", "br")]
+    rel = {n: [] for n in names}
+    lf = 0
+    for f, o in done:
+        lf += int(o["leapfrogs"].sum())
+        mc = np.nanmean(o["draws"][:, W:, :], axis=(0, 1))
+        g = gpu_outs[f]
+        mg = np.nanmean(g.draws[:, g.warmup_saved:, :], axis=(0, 1))
+        for n in names:
+            j = cols.index(n)
+            rel[n].append(abs(mg[j] - mc[j]) / abs(mc[j]))
+    value = len(done) * C * S / wall
+    return {"value": round(value, 2), "unit": "draws/s", "cores": threads, "kind": "port",
+            "value_node_est": round(value * hw["node_cpus"] / threads, 2), "host": hw,
+            "sample": (f"C oracle NUTS on files 0..{len(done) - 1} of the {files} ({C} chains x "
+                       f"({W} warmup + {S} draws) each, the same chain ids, controls and seed "
+                       f"{seed} as the GPU's last step), {conc} files at a time x {C} threads "
+                       f"on this job's {threads}-CPU share of a {hw['node_cpus']}-CPU node: "
+                       f"{lf} gradients in {wall:.1f} s"),
+            "wall_s": round(wall, 2), "files": len(done),
+            "relerr": {"files": len(done),
+                       "median": {n: round(float(np.median(v)), 6) for n, v in rel.items()},
+                       "max": {n: round(float(np.max(v)), 6) for n, v in rel.items()}}}
 
 
 def strong_scaling_est(make, files, draws_per_file, ms_1):

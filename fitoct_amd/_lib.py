@@ -74,6 +74,7 @@ class PlanInfo(C.Structure):
         ("bins_per_thread", C.c_int32), ("threads_per_tile", C.c_int32),
         ("lds_bytes", C.c_int32), ("n_pad", C.c_int32), ("draws_bytes", C.c_int64),
         ("sampler", C.c_int32), ("n_devices", C.c_int32),
+        ("two_ended", C.c_int32), ("ring_records", C.c_int32), ("ring_records_in_levels", C.c_int32),
     ]
 
 
@@ -202,7 +203,7 @@ def _single_hip_runtime():
         pass
 
 
-ABI_VERSION = 5   # include/fitoct.h FITOCT_ABI_VERSION
+ABI_VERSION = 6   # include/fitoct.h FITOCT_ABI_VERSION
 
 
 def lib():

@@ -130,10 +130,16 @@ def build(force: bool = False, verbose: bool = False, sanitize: bool = False) ->
                "-I/opt/rocm/include", "-c", os.path.join(CSRC, src), "-o", obj]
         if cc != "hipcc":
             cmd.insert(1, "-D__HIP_PLATFORM_AMD__")
+        record = name.startswith("nuts_") and not sanitize
+        if record:   # per-kernel VGPR / spill / scratch remarks, kept beside the object
+            cmd.append("-Rpass-analysis=kernel-resource-usage")
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-        if verbose and r.stderr.strip():
+        if record:
+            with open(os.path.join(objdir, name + ".resources.txt"), "w") as f:
+                f.write(r.stderr)
+        elif verbose and r.stderr.strip():
             print(r.stderr, file=sys.stderr)
         return obj
 
@@ -150,6 +156,24 @@ def build(force: bool = False, verbose: bool = False, sanitize: bool = False) ->
     with open(flags_file, "w") as f:
         f.write(_flags())
     return lib
+
+
+def kernel_resources(text: str) -> dict:
+    """Parse hipcc's ``-Rpass-analysis=kernel-resource-usage`` remarks into
+    {mangled kernel name: {"VGPRs", "VGPRs Spill", "SGPRs Spill", "ScratchSize", ...}}."""
+    import re
+    cur, rows = None, {}
+    for line in text.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            rows[cur] = {}
+            continue
+        m = re.search(r"remark: +(VGPRs|AGPRs|VGPRs Spill|SGPRs|SGPRs Spill|"
+                      r"ScratchSize \[bytes/lane\]|LDS Size \[bytes/block\]): (\d+)", line)
+        if m and cur:
+            rows[cur][m.group(1).split(" [")[0]] = int(m.group(2))
+    return rows
 
 
 if __name__ == "__main__":

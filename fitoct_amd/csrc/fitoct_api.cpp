@@ -805,7 +805,10 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
     const int ra = lvl_doubles(pl->ppl, k.max_depth) / rec;
     int rb = std::min(256, ra + (avail > 0 ? avail / (2 * rec * 8) : 0));
     if (const char* e = getenv("FITOCT_BIDI_RB")) rb = std::min(rb, std::max(1, atoi(e)));
-    if (rb >= 4 || (getenv("FITOCT_BIDI_RB") && rb >= 1)) {
+    // the three chain areas alone must fit, else the tile stays on the one-ended path (at
+    // Nn 16..24 a chain area holds two parameters per lane: three of them at max_treedepth
+    // 10 take ~181 KB of the 160 KB)
+    if (avail >= 0 && (rb >= 4 || (getenv("FITOCT_BIDI_RB") && rb >= 1))) {
       k.bidi = 1;
       k.bidi_rb = rb;
       k.bidi_rba = std::min(ra, rb);
@@ -839,6 +842,9 @@ int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
     info->lds_bytes = pl->lds;
     info->n_pad = pl->kp.n_pad;
     info->draws_bytes = (int64_t)pl->draws_bytes;
+    info->two_ended = pl->kp.bidi;
+    info->ring_records = pl->kp.bidi ? pl->kp.bidi_rb : 0;
+    info->ring_records_in_levels = pl->kp.bidi ? pl->kp.bidi_rba : 0;
     return FITOCT_OK;
   });
 }
@@ -1082,31 +1088,12 @@ int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
     std::vector<int> st(C);
     HIP_TRY(hipMemcpy(st.data(), k.chain_status, sizeof(int) * C, hipMemcpyDeviceToHost));
     if (res->chain_status) memcpy(res->chain_status, st.data(), sizeof(int) * C);
-    // A chain that timed out may have left a speculative booking in flight while it wrote
-    // its final state, so its warm-restart outputs could be torn: they are reported as NaN
-    // (fitoct_plan_set_init rejects them).  Done here, not in the kernel: any code added to
-    // the sampler's finishing action moved the headline kernel's layout and cost 2 %
-    // (profiles/r04_ab_regression.txt).
-    for (int c = 0; c < C; ++c)
-      if (st[c] == FITOCT_E_TIMEOUT) {
-        if (res->stepsize) res->stepsize[c] = NAN;
-        for (int j = 0; j < D; ++j) {
-          if (res->inv_metric) res->inv_metric[(size_t)c * D + j] = NAN;
-          if (res->last_q) res->last_q[(size_t)c * D + j] = NAN;
-        }
-      }
+    const int bad = chain_outcome(C, D, st.data(), res->stepsize, res->inv_metric, res->last_q);
     std::vector<long long> lf(C);
     HIP_TRY(hipMemcpy(lf.data(), k.leapfrogs, sizeof(long long) * C, hipMemcpyDeviceToHost));
     long long tot = 0;
     for (long long v : lf) tot += v;
     res->total_leapfrogs = tot;
-    // a chain's own failure is reported before the cancellations it may have caused
-    // (a multi-device plan cancels the other devices' chains when one fails)
-    int bad = -1;
-    for (int c = 0; c < C && bad < 0; ++c)
-      if (st[c] != 0 && st[c] != FITOCT_E_CANCELLED) bad = c;
-    for (int c = 0; c < C && bad < 0; ++c)
-      if (st[c] != 0) bad = c;
     if (bad >= 0)
       return fail(st[bad], "chain " + std::to_string(k.chain_offset + bad) + " failed with status " +
                                std::to_string(st[bad]));

@@ -425,4 +425,35 @@ extern "C" int32_t fitoct_mono_initial_theta(int32_t N, const double* x, const d
   }
 }
 
+int fitoct::chain_outcome(int C, int D, const int* st, double* eps, double* minv, double* q) {
+  // A chain that timed out may have left a speculative booking in flight while it wrote
+  // its final state, so its warm-restart outputs could be torn: they are reported as NaN
+  // (fitoct_plan_set_init rejects them).  Done on the host, not in the kernel: any code
+  // added to the sampler's finishing action moved the headline kernel's layout and cost
+  // 2 % (profiles/r04_ab_regression.txt).
+  for (int c = 0; c < C; ++c)
+    if (st[c] == FITOCT_E_TIMEOUT) {
+      if (eps) eps[c] = NAN;
+      for (int j = 0; j < D; ++j) {
+        if (minv) minv[(size_t)c * D + j] = NAN;
+        if (q) q[(size_t)c * D + j] = NAN;
+      }
+    }
+  // a chain's own failure is reported before the cancellations it may have caused
+  // (a multi-device plan cancels the other devices' chains when one fails)
+  for (int c = 0; c < C; ++c)
+    if (st[c] != 0 && st[c] != FITOCT_E_CANCELLED) return c;
+  for (int c = 0; c < C; ++c)
+    if (st[c] != 0) return c;
+  return -1;
+}
+
+// Not in include/fitoct.h: the host bookkeeping of fitoct_plan_download, exported for the
+// CPU test suite (tests/test_abi.py), which cannot make a kernel time out.
+extern "C" int32_t fitoct_internal_chain_outcome(int32_t C, int32_t D, const int32_t* status,
+                                                 double* stepsize, double* inv_metric,
+                                                 double* last_q) {
+  return fitoct::chain_outcome(C, D, status, stepsize, inv_metric, last_q);
+}
+
 extern "C" const char* fitoct_last_error(void) { return fitoct::g_last_error.c_str(); }

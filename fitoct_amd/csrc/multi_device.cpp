@@ -345,13 +345,12 @@ int group_plan_wait(fitoct_plan* pl) {
       if (k != r) (void)fitoct_plan_cancel(pl->shards[k]);
   };
   DeviceRestore keep;
-  const int rc = on_devices(n, [&](int r) -> int {
+  // every error return of a device's part (its wait, the status read, the peer copy of its
+  // block) cancels the other devices: "a failure on one device cancels the others"
+  auto part = [&](int r) -> int {
     fitoct_plan* sh = pl->shards[r];
     const int e = fitoct_plan_wait(sh);
-    if (e) {
-      cancel_others(r);
-      return e;
-    }
+    if (e) return e;
     // a failed chain (non-finite init, step-size search) fails the whole call: the other
     // devices' chains stop at their next transition boundary instead of running on
     std::vector<int> st(sh->kp.chains);
@@ -367,6 +366,11 @@ int group_plan_wait(fitoct_plan* pl) {
       HIP_TRY(hipMemcpyPeer((char*)pl->gather_dst + chain_bytes(sh) * (size_t)pl->shard_off[r],
                             pl->gather_dev, sh->last_draws, sh->cfg.device, sh->draws_bytes));
     return FITOCT_OK;
+  };
+  const int rc = on_devices(n, [&](int r) -> int {
+    const int e = part(r);
+    if (e) cancel_others(r);
+    return e;
   });
   pl->kernel_ms = 0.0;
   for (const fitoct_plan* sh : pl->shards) pl->kernel_ms = std::max(pl->kernel_ms, sh->kernel_ms);
@@ -493,7 +497,8 @@ int group_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
     for (int k = 0; k < n; ++k)
       if (k != r) __atomic_store_n(b->subs[k]->h_cancel, 1, __ATOMIC_SEQ_CST);
   };
-  const int rc = on_devices(n, [&](int r) -> int {
+  // (every error return of a device's part cancels the other devices, the peer copy's too)
+  auto part = [&](int r) -> int {
     fitoct_batch* sb = b->subs[r];
     char* slice = d_draws ? (char*)d_draws + b->per_bytes * (size_t)b->sub_off[r] : nullptr;
     const bool direct = in_place(d_draws, sb->cfg.device, gdev);
@@ -506,15 +511,12 @@ int group_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
       if (e) return e;
     }
     // FITOCT_TEST_FAIL_ENTRY=r (tests only): device entry r fails before its launch, so
-    // one GPU can exercise the cancellation of the other entries
-    static const char* inject = getenv("FITOCT_TEST_FAIL_ENTRY");
-    int e = (inject && atoi(inject) == r)
-                ? fail(FITOCT_E_INTERNAL, "injected failure (FITOCT_TEST_FAIL_ENTRY)")
-                : batch_run_single(sb, direct ? slice : nullptr, sb->own_stream);
-    if (e) {   // the call fails: the other devices' chains stop at their next checked boundary
-      cancel_others(r);
-      return e;
-    }
+    // one GPU can exercise the cancellation of the other entries (read on every call)
+    const char* inject = getenv("FITOCT_TEST_FAIL_ENTRY");
+    const int e = (inject && atoi(inject) == r)
+                      ? fail(FITOCT_E_INTERNAL, "injected failure (FITOCT_TEST_FAIL_ENTRY)")
+                      : batch_run_single(sb, direct ? slice : nullptr, sb->own_stream);
+    if (e) return e;   // the call fails: the other devices' chains stop at their next checked boundary
     // A failed chain of one file (non-finite init, step-size search) is that file's status
     // at download, as in a one-device batch: files are independent fits (FitOCT.R:70-124)
     // and the other files, on this device or another, run on.
@@ -522,6 +524,11 @@ int group_batch_run(fitoct_batch* b, void* d_draws, void* stream) {
       HIP_TRY(hipMemcpyPeer(slice, gdev, sb->d_draws, sb->cfg.device,
                             b->per_bytes * sb->plans.size()));
     return FITOCT_OK;
+  };
+  const int rc = on_devices(n, [&](int r) -> int {
+    const int e = part(r);
+    if (e) cancel_others(r);
+    return e;
   });
   b->kernel_ms = 0.0;
   for (const fitoct_batch* sb : b->subs) b->kernel_ms = std::max(b->kernel_ms, sb->kernel_ms);

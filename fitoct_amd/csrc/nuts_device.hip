@@ -176,7 +176,27 @@ constexpr int BD_GEN_MASK = (1 << 15) - 1;
 #define FITOCT_BIDI_LOOK 3   // a producer runs at most this many doublings past the booked one
 #endif
 
-constexpr long long SPIN_LIMIT = 1LL << 26;   // polls per wait (~2 s): bounded, never hang a box
+constexpr long long SPIN_LIMIT = 1LL << 26;   // polls (~2 s) before a wait reads the clock
+constexpr unsigned long long TICKS_PER_S = 100000000ULL;   // s_memrealtime: 100 MHz
+// a wait for one leaf's work (a sweep, a booking, a producer's record): far above any real
+// leaf (microseconds; a deep tree's whole trajectory is bounded separately, MIG_WAIT_TICKS)
+constexpr unsigned long long LEAF_WAIT_TICKS = 30ULL * TICKS_PER_S;
+
+// The hang guard of every wait in the kernel.  The first SPIN_LIMIT polls read no clock;
+// past them the wait is bounded in REAL time (s_memrealtime), not in polls, so a slow
+// sweep, a profiler or a deep tree never fails a healthy chain with ERR_TIMEOUT, and a
+// fault still ends the launch.  expired(T) is true once T ticks passed since poll SPIN_LIMIT.
+struct Patience {
+  long long n = 0;
+  unsigned long long t0 = 0;
+  __device__ __forceinline__ bool expired(unsigned long long ticks) {
+    if (++n <= SPIN_LIMIT) return false;
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (n == SPIN_LIMIT + 1) t0 = t;
+    __builtin_amdgcn_s_sleep(32);
+    return t - t0 > ticks;
+  }
+};
 
 __device__ __forceinline__ void wave_fence() {
   // orders this wave's LDS traffic: every earlier ds_* op has completed and the
@@ -223,7 +243,7 @@ struct MigView {   // KParams::mig carved per MigCtrl
       : hdr((AS_GLB int*)base), load((AS_GLB int*)base + MIG_HDR), fmask(load + tiles),
         mbox(fmask + tiles) {}
 };
-constexpr unsigned long long MIG_WAIT_TICKS = 120ULL * 100000000ULL;   // 120 s at 100 MHz
+constexpr unsigned long long MIG_WAIT_TICKS = 120ULL * TICKS_PER_S;
 
 // ---------------------------------------------------------------------------
 // cross-lane moves of doubles without LDS (DPP row ops, gfx950 permlane swaps)
@@ -1006,6 +1026,9 @@ struct Chain {
   int book_want = 0;
   // two-ended trajectories (P.bidi, deep tiles): the producer waves' chain areas (slots 1, 2:
   // backward, forward) and the tile's hand-off words BD_*
+  // (compiled only where it can run: a migrating tile never has the spare waves, and the
+  // two-ended code in its kernel costs the headline instantiation a spilled VGPR)
+  static constexpr bool kTwoEnded = SPEC && !MIG && FITOCT_DEEP_SPEC;
   bool bidi = false;
   AS_LDS double* pvb[2] = {nullptr, nullptr};
   AS_LDS ChainScalars* psp[2] = {nullptr, nullptr};
@@ -1023,7 +1046,7 @@ struct Chain {
     helped = SPEC && !MIG && nct_ == 1;
     deep = FITOCT_DEEP_SPEC && helped;
     HX = L.hx();
-    bidi = deep && P_.bidi != 0;
+    bidi = kTwoEnded && deep && P_.bidi != 0;
     if (bidi) {
       pvb[0] = L.vecs(1);
       pvb[1] = L.vecs(2);
@@ -1700,7 +1723,9 @@ struct Chain {
 
   __device__ int act_begin_subtree() {
     FITOCT_MARK(act_begin_subtree);
-    if (bidi) return bidi_begin();   // reached at depth 0 only: the helper books from there on
+    if constexpr (kTwoEnded) {
+      if (bidi) return bidi_begin();   // reached at depth 0 only: the helper books from there on
+    }
     const int d = uni(Sp->depth);
     const double u = uniform(key, (uint32_t)uni(Sp->t), TAG_DIR, (uint32_t)d, 0u);
     const int dir = (u > 0.5) ? 1 : 0;
@@ -1893,9 +1918,9 @@ struct Chain {
   __device__ int wait_booking() {
     if (book_want == 0) return LB_MID;
     long long ts = stamp0();   // profiling build: sub-stamp 8 = this wave's stall on the booking
-    long long spins = 0;
+    Patience w;
     while (*book_done < book_want) {
-      if (++spins > SPIN_LIMIT) {
+      if (w.expired(LEAF_WAIT_TICKS)) {
         Sp->status = ERR_TIMEOUT;
         return -1;
       }
@@ -2094,9 +2119,9 @@ struct Chain {
     sub(2, ts);
     // phase B: the helper's weight of this leaf (or this wave's own, act_spec_book)
     if (helped && !deep) {
-      long long spins = 0;
+      Patience w;
       while (*help_wdone < help_want) {
-        if (++spins > SPIN_LIMIT) {
+        if (w.expired(LEAF_WAIT_TICKS)) {
           Sp->status = ERR_TIMEOUT;
           return LB_END;
         }
@@ -2476,7 +2501,7 @@ struct Chain {
       }
       asm volatile("" : "+s"(a), "+s"(pp));
       if (a == A_YIELD || a == A_SPEC_STAGED || a == A_SPEC_WAIT || a == A_SPEC_DISCARD ||
-          a == A_BIDI_TREE)
+          (kTwoEnded && a == A_BIDI_TREE))
         break;
       const bool prof = kProfile && Pr().stamps != nullptr;
       const long long t0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -2641,7 +2666,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   __shared__ int help_req, help_done, help_wdone, help_arg[3], help_res;
   const bool spec = SPEC;
   const bool helped = SPEC && !MIG && nct == 1;   // a spare NUTS wave helps the tile's one chain
-  const bool bidi = helped && FITOCT_DEEP_SPEC && P.bidi != 0;   // ... and two producer waves
+  const bool bidi = Chain<PPL, NNP, FAM, MIG, SPEC>::kTwoEnded && helped &&
+                   P.bidi != 0;   // ... and two producer waves
   __shared__ int live_chains;   // chains the tile hosts (speculation policy, Chain::live)
 
   load_kinv<PPL, NNP>(P, L, tid);
@@ -2692,11 +2718,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     Bins<R, BPT, NNP, MODE> bins;
     bins.load(P, tid);
     int zero_done[GMAX] = {0, 0, 0, 0};
-    unsigned long long t_idle = 0;
     for (unsigned h = 0;; ++h) {
       unsigned long long e;
       bool stop = false;
-      long long spins = 0;
+      Patience w;
       for (;;) {  // wait for ring entry h
         e = lds_load64(&ring[h % RINGN]);
         if ((unsigned)(e >> 32) == h) break;
@@ -2704,19 +2729,12 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           stop = true;
           break;
         }
-        // hang guard: with migration a tile may idle (receivers posted) until
-        // the launch's last chain ends, so the bound is in time, not polls
-        if (++spins > SPIN_LIMIT) {
-          if (!MIG || P.mig == nullptr) {
-            stop = true;
-            break;
-          }
-          if (spins == SPIN_LIMIT + 1) t_idle = __builtin_amdgcn_s_memrealtime();
-          if (__builtin_amdgcn_s_memrealtime() - t_idle > MIG_WAIT_TICKS + 1000000000ULL) {
-            stop = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(32);
+        // hang guard: with migration a tile may idle (receivers posted) until the launch's
+        // last chain ends; without, its chains may pause between sweeps (a two-ended tree's
+        // chain wave, init) but never for a leaf's wait bound
+        if (w.expired(MIG_WAIT_TICKS + 10 * TICKS_PER_S)) {
+          stop = true;
+          break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
@@ -2762,17 +2780,12 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       int seen = 0;
       for (;;) {
         int g;
-        long long spins = 0;
-        unsigned long long t_idle = 0;
+        Patience w;   // (init and step-size searches run between transitions)
         bool quit = false;
         while ((g = lds_load(&bd[BD_GEN])) == seen) {   // the next transition, or the end
-          if (++spins > SPIN_LIMIT) {   // hang guard in real time (init, step-size searches)
-            if (spins == SPIN_LIMIT + 1) t_idle = __builtin_amdgcn_s_memrealtime();
-            if (__builtin_amdgcn_s_memrealtime() - t_idle > MIG_WAIT_TICKS) {
-              quit = true;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(32);
+          if (w.expired(MIG_WAIT_TICKS)) {
+            quit = true;
+            break;
           }
           __builtin_amdgcn_s_sleep(1);
         }
@@ -2783,18 +2796,19 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         for (;;) {
           const int s = ch.uni(ch.Sp->dir);   // the subtree being booked grows this end
           const int n = s ? cons1 : cons0;
-          long long sp = 0;
+          bool lost = false;
+          Patience wl;   // one producer leaf: its throttle never holds back the leaf booked next
           for (;;) {   // leaf n of stream s published for this transition
             const int w = lds_load(&bd[BD_PROD + s]);
             if ((w >> 16) == g && (w & 0xFFFF) > n) break;
-            if (++sp > SPIN_LIMIT || lds_load(&bd[BD_GEN]) != g) {   // never, short of a fault
-              sp = SPIN_LIMIT + 1;
+            if (lds_load(&bd[BD_GEN]) != g || wl.expired(LEAF_WAIT_TICKS)) {   // never, short of a fault
+              lost = true;
               break;
             }
             __builtin_amdgcn_s_sleep(1);
           }
           int r = Ch::LB_END;
-          if (sp > SPIN_LIMIT) {
+          if (lost) {
             ch.Sp->status = ERR_TIMEOUT;
           } else {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the record after its count
@@ -2823,16 +2837,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       while (!quit) {
         int g;
         {
-          long long spins = 0;
-          unsigned long long t_idle = 0;
+          Patience w;
           while ((g = lds_load(&bd[BD_GEN])) == seen) {
-            if (++spins > SPIN_LIMIT) {
-              if (spins == SPIN_LIMIT + 1) t_idle = __builtin_amdgcn_s_memrealtime();
-              if (__builtin_amdgcn_s_memrealtime() - t_idle > MIG_WAIT_TICKS) {
-                quit = true;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(32);
+            if (w.expired(MIG_WAIT_TICKS)) {
+              quit = true;
+              break;
             }
             __builtin_amdgcn_s_sleep(1);
           }
@@ -2861,8 +2870,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         int n = 0;
         for (;;) {
           bool go = false;
-          long long spins = 0;
-          unsigned long long t_thr = 0;
+          Patience w;
           for (;;) {   // within FITOCT_BIDI_LOOK doublings of the booked one, and the ring
             if (lds_load(&bd[BD_GEN]) != g) break;
             const int dl = min(pr.uni(*(volatile const AS_LDS int*)&S0.depth) + FITOCT_BIDI_LOOK,
@@ -2873,12 +2881,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
               go = true;
               break;
             }
-            // the other end may grow for long (deep trees, large N): bounded in real time
-            if (++spins > SPIN_LIMIT) {
-              if (spins == SPIN_LIMIT + 1) t_thr = __builtin_amdgcn_s_memrealtime();
-              if (__builtin_amdgcn_s_memrealtime() - t_thr > MIG_WAIT_TICKS) break;
-              __builtin_amdgcn_s_sleep(32);
-            }
+            // the other end may grow for long (deep trees, large N).  In effect this wait
+            // ends with BD_GEN: its bound outlasts the chain wave's bound on the whole tree
+            // (MIG_WAIT_TICKS from the tree's start), after which BD_GEN changes
+            if (w.expired(2 * MIG_WAIT_TICKS)) break;
             __builtin_amdgcn_s_sleep(1);
           }
           if (!go) break;   // the tree ended (next transition or the end)
@@ -2897,12 +2903,16 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           }
           ++epoch;
           pr.prior_part();   // overlaps the sweep
-          long long ws = 0;
+          bool late = false;
+          Patience ws;
           while (lds_load(&grad_cnt[slot]) < (int)(NGW * epoch)) {
-            if (++ws > SPIN_LIMIT) break;
+            if (ws.expired(LEAF_WAIT_TICKS)) {
+              late = true;
+              break;
+            }
             __builtin_amdgcn_s_sleep(1);
           }
-          if (ws > SPIN_LIMIT) {
+          if (late) {
             quit = true;
             break;
           }
@@ -2944,8 +2954,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
       Ch ch(P, L, 0, c0, lane, nct);
       int seen = 0;
-      long long spins = 0;
-      unsigned long long t_idle = 0;
+      Patience w;
       for (;;) {
         const int r = lds_load(&help_req);
         if (r < 0) break;                       // the chain has finished
@@ -2953,15 +2962,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           // the chain releases its helper when it finishes (help_req = -1), however long
           // its gaps between speculated leaves (init, step-size searches): the hang guard
           // is in real time, not polls, as for migration receivers
-          if (++spins > SPIN_LIMIT) {
-            if (spins == SPIN_LIMIT + 1) t_idle = __builtin_amdgcn_s_memrealtime();
-            if (__builtin_amdgcn_s_memrealtime() - t_idle > MIG_WAIT_TICKS) break;
-            __builtin_amdgcn_s_sleep(32);
-          }
+          if (w.expired(MIG_WAIT_TICKS)) break;
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
-        spins = 0;
+        w = Patience{};
         seen = r;
         wave_fence();   // the request's arguments are read after its number
         if (ch.deep) {   // book the handed-over leaf; publish its outcome, then the number
@@ -3004,26 +3009,23 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if (lowp) __builtin_amdgcn_s_setprio(FITOCT_DEEP_PRIOR_PRIO);
         const int y = ch.run(a);
         if (lowp) __builtin_amdgcn_s_setprio(3);
-        if (spec && y == Ch::A_BIDI_TREE) {   // the producers and the helper grow the tree
+        if (Ch::kTwoEnded && y == Ch::A_BIDI_TREE) {   // the producers and the helper grow the tree
           const int g = lds_load(&bd[BD_GEN]);
-          long long spins = 0;
-          unsigned long long t_tree = 0;
+          Patience w;
           bool late = false;
           if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_BIDI_IDLE_PRIO);
-          while (lds_load(&bd[BD_END]) != g) {   // a whole tree: bounded in real time
-            if (++spins > SPIN_LIMIT) {
-              if (spins == SPIN_LIMIT + 1) t_tree = __builtin_amdgcn_s_memrealtime();
-              if (__builtin_amdgcn_s_memrealtime() - t_tree > MIG_WAIT_TICKS) {
-                late = true;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(32);
+          while (lds_load(&bd[BD_END]) != g) {   // a whole tree
+            if (w.expired(MIG_WAIT_TICKS)) {
+              late = true;
+              break;
             }
             __builtin_amdgcn_s_sleep(FITOCT_BIDI_IDLE_SLEEP);
           }
           if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
           wave_fence();   // the helper's bookkeeping is read after the end
-          if (late || ch.uni(ch.Sp->status) == ERR_TIMEOUT) {
+          // the helper's booked leaves count toward the step bound like the chain's own
+          steps += ch.uni(ch.Sp->n_leapfrog);
+          if (late || ch.uni(ch.Sp->status) == ERR_TIMEOUT || steps > P.max_steps) {
             ch.Sp->status = ERR_TIMEOUT;
             a = Ch::A_FINISH;
           } else {
@@ -3073,11 +3075,15 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           continue;
         }
         if (spec && (y == Ch::A_SPEC_WAIT || y == Ch::A_SPEC_DISCARD)) {
-          long long spins = 0;
+          bool late = false;
+          Patience w;
           const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
           if (stamp) t_busy += w0 - s0;
           while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch) || lds_load(&help_done) < hreq) {
-            if (++spins > SPIN_LIMIT) break;
+            if (w.expired(LEAF_WAIT_TICKS)) {
+              late = true;
+              break;
+            }
             __builtin_amdgcn_s_sleep(1);
           }
           wave_fence();   // nothing of the next action is read before the sweep and the helper are done
@@ -3092,7 +3098,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             t_notice += t1 - (done_t[c] > w0 ? done_t[c] : w0);
             ++n_items;
           }
-          if (spins > SPIN_LIMIT) {
+          if (late) {
             ch.Sp->status = ERR_TIMEOUT;
             a = Ch::A_FINISH;
           } else {
@@ -3102,7 +3108,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         }
         if (in_sweep) {
           in_sweep = false;
-          long long spins = 0;
+          bool late = false;
+          Patience w;
           const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
           // A NUTS wave waits at priority 3 on a SIMD it shares with a gradient wave.  When
           // the sweep is long (8+ bins per lane, or streamed bins) and the tile hosts
@@ -3111,13 +3118,19 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           if (P.G >= 2 && (BPT >= 8 || BPT == 0)) {
             if (FITOCT_NUTS_WAIT_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_NUTS_WAIT_PRIO);
             while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
-              if (++spins > SPIN_LIMIT) break;
+              if (w.expired(LEAF_WAIT_TICKS)) {
+                late = true;
+                break;
+              }
               __builtin_amdgcn_s_sleep(FITOCT_NUTS_POLL);
             }
             if (FITOCT_NUTS_WAIT_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
           } else {
             while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
-              if (++spins > SPIN_LIMIT) break;
+              if (w.expired(LEAF_WAIT_TICKS)) {
+                late = true;
+                break;
+              }
               __builtin_amdgcn_s_sleep(1);
             }
           }
@@ -3131,7 +3144,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             start_max[c] = 0;
             t_notice += t1 - (done_t[c] > w0 ? done_t[c] : w0);
           }
-          if (spins > SPIN_LIMIT) {
+          if (late) {
             ch.Sp->status = ERR_TIMEOUT;
             a = Ch::A_FINISH;
           } else {
@@ -3153,8 +3166,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           if (helped && lane == 0) __atomic_store_n(&help_req, -1, __ATOMIC_RELAXED);   // release the helper
           if (bidi) {   // release the producers and the helper; the producers drain their sweeps
             if (lane == 0) __atomic_store_n(&bd[BD_GEN], -1, __ATOMIC_RELAXED);
-            long long spins = 0;
-            while (lds_load(&bd[BD_EXIT]) < 2 && ++spins < SPIN_LIMIT) __builtin_amdgcn_s_sleep(1);
+            Patience w;
+            while (lds_load(&bd[BD_EXIT]) < 2 && !w.expired(LEAF_WAIT_TICKS)) __builtin_amdgcn_s_sleep(1);
           }
           if (spec && lane == 0) atomicSub(&live_chains, 1);
           break;

@@ -53,6 +53,21 @@ def rank_rhat(x: np.ndarray) -> float:
     return r.value
 
 
+def trapped_chains(divergent: np.ndarray) -> np.ndarray:
+    """The fixed definition of a funnel-trapped chain used by bench.py's lines and the
+    tests: more than half of its post-warmup transitions diverge over the
+    run or over either half of it (a chain can fall into the horseshoe funnel's neck
+    mid-run and stay there).  divergent[chains, draws] (the divergent__ column) -> bool
+    [chains].  ``trapped_whole_run`` is the rule of rounds 1-3 (whole run only)."""
+    d = np.asarray(divergent, dtype=np.float64)
+    h = d.shape[1] // 2
+    return (d.mean(1) > 0.5) | (d[:, :h].mean(1) > 0.5) | (d[:, h:].mean(1) > 0.5)
+
+
+def trapped_whole_run(divergent: np.ndarray) -> np.ndarray:
+    return np.asarray(divergent, dtype=np.float64).mean(1) > 0.5
+
+
 def output_columns(prob, lead=SAMPLER_COLS) -> list:
     """Column names of the output layout (include/fitoct.h, "Stan output"): the
     leading columns, the model's parameters, the transformed parameters of the

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FITOCT_ABI_VERSION 5
+#define FITOCT_ABI_VERSION 6
 /* largest accepted N (depth bins): bounds every host and device allocation derived from it */
 #define FITOCT_MAX_BINS (1 << 22)
 /* largest device list of one call (fitoct_config.devices) */
@@ -160,6 +160,14 @@ typedef struct fitoct_plan_info {
   int64_t draws_bytes;     /* size of the draws buffer */
   int32_t sampler;         /* sampler variant launched: FITOCT_SAMPLER_* */
   int32_t n_devices;       /* devices the plan's chains (a batch's problems) run on */
+  /* ABI 6: two-ended trajectories (tiles of one chain grow the trajectory's backward and
+   * forward ends on two spare waves at once; same draws bit for bit).  two_ended = 1 when
+   * the plan's one-chain tiles run them; ring_records = leaf records per end's LDS ring,
+   * ring_records_in_levels = how many of them sit in the producer's tree-level area (the
+   * rest extend the LDS carve); both 0 when off. */
+  int32_t two_ended;
+  int32_t ring_records;
+  int32_t ring_records_in_levels;
 } fitoct_plan_info;
 
 /* fitoct_plan_info::sampler.  PLAIN: no speculation, no migration;

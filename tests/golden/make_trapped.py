@@ -17,8 +17,16 @@ every parameter column the two half-chain means and variances (split R-hat of an
 chain subset follows from them) plus the single-chain Geyer ESS (bulk, of the
 post-warmup draws).  No draws are stored.
 
-Run:  python tests/golden/make_trapped.py [headline|lasso|all] [--threads T]
-(deterministic; ~40 min for the headline case on 8 cores, ~15 min for lasso).
+The ``batch`` case (config 5, FitOCT.R's batch mode) is per FILE instead: the 256
+synthetic files of bench.py's config-5 line (the four synthData.R modulations cycled, data
+seeds 1234 + f, N = 481, normal prior), 4 chains each with global ids 4f .. 4f + 3, at
+ctrlParams.yaml:1-2's 100 warmup + 100 draws and bench step 0's seed 2000.  Stored per
+file: the max split R-hat over the parameter columns (the config-5 line's statistic; the
+Shiny app paints R-hat >= 1.1 red, ShinyInterface/server.R:98-100), the chains' mean
+adapted step size, tree depth and divergence rate (``batch_files.npz``).
+
+Run:  python tests/golden/make_trapped.py [headline|lasso|batch|all] [--threads T]
+(deterministic; ~40 min for the headline case on 8 cores, ~15 min for lasso, ~1 min batch).
 """
 from __future__ import annotations
 
@@ -124,6 +132,58 @@ def make(name, threads):
           f"median div {np.median(out['div_rate']):.4f}", flush=True)
 
 
+# config 5 (bench.py CONFIGS[5], bench_batch): files, N, chains per file, W, S, seed
+BATCH = dict(files=256, N=481, chains=4, warmup=100, samples=100, seed=2000, adapt_delta=0.8,
+             max_treedepth=10)
+
+
+def batch_problem(f):
+    """bench.py:bench_batch's file_problems(f, 1), restated (no bench.py import)."""
+    from fitoct_amd import ExpGPProblem
+    from fitoct_amd.synth import MODULATIONS, default_prior, synth_decay
+    t0, S0 = default_prior()
+    d = synth_decay(BATCH["N"], MODULATIONS[f % 4], 1234 + f)
+    return ExpGPProblem(d["x"], d["y"], d["uy"], dataType=2, Nn=15, gridType="extremal",
+                        theta0=t0, Sigma0=S0, prior_type="normal")
+
+
+def file_stats(draws, W, cols):
+    """One file's draws[chains, W + S, n_cols] -> (max split R-hat over the parameter
+    columns, mean step size, mean tree depth, divergence rate), with oracle/diag_np."""
+    from oracle.diag_np import split_rhat
+    post = np.asarray(draws[:, W:, :], dtype=np.float64)
+    rh = max(split_rhat(post[:, :, j]) for j in param_columns(cols))
+    return (float(rh), float(post[:, 0, 2].mean()), float(post[:, :, 3].mean()),
+            float(post[:, :, 5].mean()))
+
+
+def make_batch(threads):
+    from fitoct_amd import SamplerConfig
+    from oracle import nuts_c
+    B = BATCH
+    C = B["chains"]
+    rows = []
+    t = time.time()
+    for f in range(B["files"]):
+        prob = batch_problem(f)
+        cfg = SamplerConfig(chains=C, chain_offset=f * C, warmup=B["warmup"],
+                            samples=B["samples"], seed=B["seed"], adapt_delta=B["adapt_delta"],
+                            max_treedepth=B["max_treedepth"])
+        o = nuts_c.sample(prob, cfg, nthreads=min(threads, C))
+        rows.append(file_stats(o["draws"], B["warmup"], prob.column_names()))
+        if f % 32 == 31:
+            print(f"[batch] files [0, {f + 1}) done, {time.time() - t:.0f} s", flush=True)
+    a = np.array(rows)
+    meta = dict(case="batch", prior="normal", modulations="synthData.R sincExp..sincExp3 cycled",
+                data_seed="1234 + file", chain_ids="4 file + c", Nn=15,
+                generator="oracle/fitoct_oracle.c via oracle/nuts_c.py", **B)
+    path = os.path.join(HERE, "batch_files.npz")
+    np.savez_compressed(path, meta=np.array(json.dumps(meta)), rhat_max=a[:, 0],
+                        stepsize=a[:, 1], treedepth=a[:, 2], div_rate=a[:, 3])
+    print(f"[batch] wrote {path}: median max R-hat {np.median(a[:, 0]):.4f}, "
+          f"files >= 1.1: {int((a[:, 0] >= 1.1).sum())}/{len(a)}", flush=True)
+
+
 def load(path):
     with np.load(path, allow_pickle=False) as z:
         out = {k: z[k] for k in z.files}
@@ -133,8 +193,10 @@ def load(path):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("case", nargs="?", default="all", choices=["all", *CASES])
+    ap.add_argument("case", nargs="?", default="all", choices=["all", "batch", *CASES])
     ap.add_argument("--threads", type=int, default=8)
     a = ap.parse_args()
-    for n in (CASES if a.case == "all" else [a.case]):
+    for n in (CASES if a.case == "all" else [] if a.case == "batch" else [a.case]):
         make(n, a.threads)
+    if a.case in ("all", "batch"):
+        make_batch(a.threads)

@@ -46,7 +46,7 @@ def test_struct_layouts_match_ctypes():
     sizes = _lib.struct_sizes()
     assert sizes == (C.sizeof(_lib.Problem), C.sizeof(_lib.Config), C.sizeof(_lib.Result),
                      C.sizeof(_lib.PlanInfo))
-    assert _lib.lib().fitoct_abi_version() == 5 == _lib.ABI_VERSION
+    assert _lib.lib().fitoct_abi_version() == 6 == _lib.ABI_VERSION
 
 
 def test_default_config_is_stan_default():
@@ -324,3 +324,35 @@ def test_theta_prior_oracles_agree():
                 assert lp_n == pytest.approx(q[i].sum() - th.sum() / 10.0, rel=1e-12)
             else:
                 assert lp_n - lp_f == pytest.approx(-th.sum() / 10.0, rel=1e-10)
+
+
+@pytest.mark.parametrize("status,report", [
+    ([0, 0, 0], -1),
+    ([0, -6, 0], 1),                 # a timeout
+    ([-8, -8, -6, -8], 2),           # its own failure before the cancellations it caused
+    ([-8, 0, -8], 0),                # cancelled only (fitoct_plan_cancel)
+    ([0, -4, -6], 1),                # the first own failure (init) wins
+])
+def test_chain_outcome_timeout_bookkeeping(status, report):
+    """fitoct_plan_download's host bookkeeping (no kernel needed): a chain whose status is
+    FITOCT_E_TIMEOUT (a real-time bounded wait in the kernel expired) reports NaN
+    warm-restart outputs (fitoct_plan_set_init rejects a non-finite start); every other chain's outputs
+    are left as the kernel wrote them; the call reports the first chain's own failure
+    before any cancellation."""
+    L = _lib.lib()
+    f = L.fitoct_internal_chain_outcome
+    f.restype = C.c_int32
+    Cn, D = len(status), 3
+    st = np.array(status, dtype=np.int32)
+    eps = np.arange(1, Cn + 1, dtype=np.float64)
+    minv = np.ones((Cn, D))
+    q = np.full((Cn, D), 2.0)
+    r = f(Cn, D, st.ctypes.data_as(C.POINTER(C.c_int32)), _lib.dptr(eps), _lib.dptr(minv),
+          _lib.dptr(q))
+    assert r == report
+    tim = st == -6   # FITOCT_E_TIMEOUT
+    assert np.all(np.isnan(eps[tim])) and np.all(np.isnan(minv[tim])) and np.all(np.isnan(q[tim]))
+    assert np.all(eps[~tim] == np.arange(1, Cn + 1)[~tim])
+    assert np.all(minv[~tim] == 1.0) and np.all(q[~tim] == 2.0)
+    # NULL outputs are allowed
+    assert f(Cn, D, st.ctypes.data_as(C.POINTER(C.c_int32)), None, None, None) == report

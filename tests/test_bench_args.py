@@ -59,3 +59,27 @@ def test_convergence_counts_chains_trapped_mid_run():
     assert out["rhat_max"] > 1.1 and out["rhat_max_excl_stuck"] < 1.02
     assert out["ess_per_chain_min"] > 0
     assert [c for c, _ in out["ess_per_chain_lowest_columns"]][:1] in (["theta.1"], ["theta.2"])
+
+
+@pytest.mark.parametrize("world,visible,env,want", [
+    (8, 8, "", (0, 1, 2, 3, 4, 5, 6, 7)),   # the driver's node: one rank per GPU
+    (8, 1, "", (0,) * 8),                   # rehearsal on one GPU: visible ordinals only
+    (2, 1, "0,0", (0, 0)),
+    (4, 2, "", (0, 1, 0, 1)),
+])
+def test_device_list_leg_uses_visible_ordinals(world, visible, env, want, monkeypatch):
+    """The torchrun line's device-list sub-object (bench._dl_devices): one entry per rank,
+    each a visible ordinal, so an 8-rank rehearsal on one GPU populates it instead of
+    failing with 'device ordinal out of range' (round 4's profiles/r04_rehearse8.txt)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setenv("FITOCT_BENCH_DEVICE_LIST", env)
+    assert bench._dl_devices(world, visible) == want
+
+
+def test_device_list_leg_rejects_invisible_ordinals(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setenv("FITOCT_BENCH_DEVICE_LIST", "0,3")
+    with pytest.raises(ValueError, match="not among the 2 visible"):
+        bench._dl_devices(2, 2)

@@ -118,3 +118,47 @@ def test_lasso_slow_mixing_matches_oracle():
     for name in ("yGP.6", "yGP.7", "yGP.8"):
         j = cols.index(name)
         assert abs(math.log(rg[j] - 1) - math.log(ro[j] - 1)) < math.log(2.0), (name, rg[j], ro[j])
+
+
+def _boot_se(x, stat, n_boot=2000, seed=0):
+    rng = np.random.default_rng(seed)
+    x = np.asarray(x, float)
+    return float(np.std([stat(x[rng.integers(0, x.size, x.size)]) for _ in range(n_boot)]))
+
+
+def test_config5_file_rhat_distribution_matches_oracle():
+    """Config 5 (FitOCT.R batch mode: 256 files x 4 chains at ctrlParams.yaml:1-2's 100
+    warmup + 100 draws, bench.py's files, chain ids and step-0 seed) against the C oracle
+    on the same files (tests/golden/batch_files.npz, make_trapped.py batch).  With 4 chains
+    of 100 draws a file's max split R-hat over its ~22 columns is often above 1.1 -- the
+    Shiny app's red line (ShinyInterface/server.R:98-100) -- for the ALGORITHM, not the
+    port: the oracle has 27 / 256 such files, median 1.057.  Asserted, within the sampling
+    error of both sides (3 combined SE; medians / 90th percentiles by bootstrap): the
+    fraction of files >= 1.1, the median and 90th-percentile file R-hat, and the files'
+    mean log step size, tree depth and divergence rate."""
+    from fitoct_amd import Batch
+    fx = T.load(os.path.join(HERE, "golden", "batch_files.npz"))
+    B = fx["meta"]
+    probs = [T.batch_problem(f) for f in range(B["files"])]
+    cfg = SamplerConfig(chains=B["chains"], warmup=B["warmup"], samples=B["samples"],
+                        seed=B["seed"], adapt_delta=B["adapt_delta"],
+                        max_treedepth=B["max_treedepth"])
+    with Batch(probs, cfg) as b:
+        b.run()
+        outs = [b.download(p) for p in range(len(probs))]
+    cols = probs[0].column_names()
+    g = np.array([T.file_stats(o.draws, o.warmup_saved, cols) for o in outs])
+    rg, ro = g[:, 0], fx["rhat_max"]
+    n = len(rg)
+    assert _prop_agree(int((rg >= 1.1).sum()), n, int((ro >= 1.1).sum()), ro.size), \
+        ((rg >= 1.1).sum(), (ro >= 1.1).sum())
+    for q in (50, 90):
+        stat = (lambda x, q=q: np.percentile(x, q))
+        se = math.hypot(_boot_se(rg, stat), _boot_se(ro, stat, seed=1))
+        d = stat(rg) - stat(ro)
+        assert abs(d) <= 3 * se, (q, stat(rg), stat(ro), se)
+    for k, name in ((1, "log stepsize"), (2, "treedepth"), (3, "div_rate")):
+        a = np.log(g[:, k]) if k == 1 else g[:, k]
+        o = np.log(fx["stepsize"]) if k == 1 else fx[name]
+        ok, d, se = _mean_agree(a, o)
+        assert ok, (name, d, se)

@@ -1,0 +1,93 @@
+"""Register-allocation gate for the sampler kernels every BASELINE config launches (CPU
+suite: the compiler's own resource remarks, no GPU).
+
+A spilled VGPR in the NUTS waves' shared allocation turns into scratch loads on the
+sampler's critical path: round 3 measured one spilled VGPR at -2.2 % on the headline, and
+round 4's two-ended code (which cannot run in a migrating tile) put 2 spilled VGPRs / 12 B
+of scratch back into the headline instantiation without any test noticing.  This test
+reads the ``-Rpass-analysis=kernel-resource-usage`` remarks that ``fitoct_amd.build``
+records beside each sampler object (``fitoct_amd/build/nuts_<family>.resources.txt``) and
+asserts 0 VGPR spill and 0 scratch for each instantiation below.  If the record is missing
+or older than the kernel source, the family is recompiled device-only for the remarks.
+
+Template arguments of ``nuts_kernel``: <R, BPT (bins per lane), NNP, PPL, MODE, FAM,
+MIG (chain migration), SPEC (speculative leaves)>; the plan picks them in
+``fitoct_api.cpp`` (tiles of one chain -> MIG = false, SPEC = true; 1024 chains on 256 CUs
+-> G = 4, migration + tail speculation; batch mode -> MIG = false, SPEC = false).
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from fitoct_amd import build as B  # noqa: E402
+
+FAM_OBJ = {0: "nuts_normal", 1: "nuts_lasso", 2: "nuts_horseshoe", 3: "nuts_monoexp"}
+
+
+def mangled(bpt, fam, mig, spec, nnp=15, ppl=1, mode=0, real="d"):
+    return (f"_ZN6fitoct11nuts_kernelI{real}Li{bpt}ELi{nnp}ELi{ppl}ELi{mode}ELi{fam}E"
+            f"Lb{int(mig)}ELb{int(spec)}EEEvPKNS_7KParamsEPKi")
+
+
+# (BASELINE config, family, kernel)
+LAUNCHED = [
+    ("config 3 headline: horseshoe N=2048, 1024 chains (G=4, migrating + tail speculation)",
+     2, mangled(8, 2, True, True)),
+    ("config 3 without speculation (FITOCT_NO_SPEC)", 2, mangled(8, 2, True, False)),
+    ("config 4: lasso N=4096, 16 bins per lane, migrating + tail speculation",
+     1, mangled(16, 1, True, True)),
+    ("config 2: normal N=512, 128 chains, tiles of one chain (two-ended trajectories)",
+     0, mangled(2, 0, False, True)),
+    ("config 5 at one GPU: batch tiles of four chains, plain sampler", 0, mangled(2, 0, False, False)),
+    ("config 5 multi-GPU shares: batch tiles of one chain (speculating)", 0, mangled(2, 0, False, True)),
+]
+
+
+def _record(fam):
+    obj = FAM_OBJ[fam]
+    path = os.path.join(B.OBJDIR, obj + ".resources.txt")
+    src = os.path.join(B.CSRC, "nuts_device.hip")
+    if os.path.exists(path) and os.path.getmtime(path) >= B._newest_dep(src):
+        with open(path) as f:
+            return f.read()
+    hipcc = B._hipcc()
+    out = os.path.join("/tmp", f"fitoct_resources_{fam}_{os.getpid()}.o")
+    cmd = [hipcc, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", f"-DFITOCT_FAMILY={fam}",
+           f"-I{B.INCLUDE}", f"-I{B.CSRC}", "--cuda-device-only", "-c", src, "-o", out,
+           "-Rpass-analysis=kernel-resource-usage"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    os.remove(out)
+    return r.stderr
+
+
+_cache = {}
+
+
+def _rows(fam):
+    if fam not in _cache:
+        _cache[fam] = B.kernel_resources(_record(fam))
+    return _cache[fam]
+
+
+@pytest.mark.parametrize("what,fam,kernel", LAUNCHED, ids=[w.split(":")[0] + f"-{i}"
+                                                          for i, (w, _, _) in enumerate(LAUNCHED)])
+def test_baseline_instantiations_do_not_spill(what, fam, kernel):
+    rows = _rows(fam)
+    assert kernel in rows, f"{kernel} not compiled ({what})"
+    r = rows[kernel]
+    assert r.get("VGPRs Spill", -1) == 0, (what, r)
+    assert r.get("ScratchSize", -1) == 0, (what, r)
+    assert r.get("VGPRs", 999) <= 256, (what, r)
+
+
+def test_parser_reads_every_sampler_kernel():
+    rows = _rows(2)
+    names = [k for k in rows if "nuts_kernel" in k]
+    assert len(names) >= 24, len(names)
+    for k in names:
+        assert {"VGPRs", "VGPRs Spill", "ScratchSize"} <= set(rows[k]), (k, rows[k])

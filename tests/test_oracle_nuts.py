@@ -143,3 +143,25 @@ def test_warm_restart_restatement():
     d1 = nuts_c.sample(prob, cfg, nthreads=4)
     assert np.array_equal(d0["draws"], d1["draws"], equal_nan=True)
     assert not np.array_equal(d0["draws"], a["draws"], equal_nan=True)
+
+
+def test_batch_fixture_reproduces_from_the_committed_script():
+    """tests/golden/batch_files.npz (config 5's per-file oracle behaviour, compared with the
+    GPU in test_gpu_funnel.py) is what tests/golden/make_trapped.py computes: the first
+    files re-run here give the stored per-file R-hat, step size, depth and divergences."""
+    import sys as _s
+    _s.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_trapped as T
+    fx = T.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                             "batch_files.npz"))
+    B = fx["meta"]
+    assert (B["files"], B["chains"], B["warmup"], B["samples"]) == (256, 4, 100, 100)
+    for f in (0, 1, 2):
+        prob = T.batch_problem(f)
+        cfg = SamplerConfig(chains=B["chains"], chain_offset=f * B["chains"], warmup=B["warmup"],
+                            samples=B["samples"], seed=B["seed"], adapt_delta=B["adapt_delta"],
+                            max_treedepth=B["max_treedepth"])
+        o = nuts_c.sample(prob, cfg, nthreads=4)
+        st = T.file_stats(o["draws"], B["warmup"], prob.column_names())
+        np.testing.assert_allclose(st, [fx["rhat_max"][f], fx["stepsize"][f], fx["treedepth"][f],
+                                        fx["div_rate"][f]], rtol=1e-12)
