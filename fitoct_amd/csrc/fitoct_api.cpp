@@ -1046,6 +1046,22 @@ int32_t fitoct_plan_wait(fitoct_plan* pl) {
                 "finished %.0f, launch %.1f ms\n",
                 mean_end, q(ends, 0.1), q(ends, 0.5), q(ends, 0.9), q(firsts, 0.1), q(firsts, 0.5),
                 q(firsts, 0.9), done_sum, span / 1e5);
+        // tile occupancy: share of all tiles' time, and of all sweeps, spent while a tile
+        // hosted k live chains (k = 0..4; the launch's tail runs thinned-out tiles)
+        double ot[5] = {0}, on[5] = {0}, st = 0, sn = 0;
+        for (int t = 0; t < pl->tiles; ++t)
+          for (int k = 0; k < 5; ++k) {
+            ot[k] += h[(size_t)NSTAMP * t + 72 + k];
+            on[k] += h[(size_t)NSTAMP * t + 77 + k];
+          }
+        for (int k = 0; k < 5; ++k) {
+          st += ot[k];
+          sn += on[k];
+        }
+        fprintf(stderr, "[fitoct stamps] tile occupancy (live chains k: share of tile time / of sweeps):");
+        for (int k = 0; k < 5; ++k)
+          fprintf(stderr, " k=%d %.4f/%.4f", k, ot[k] / std::max(st, 1.0), on[k] / std::max(sn, 1.0));
+        fprintf(stderr, "\n");
       }
     }
     pl->ran = true;

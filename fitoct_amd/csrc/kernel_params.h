@@ -20,7 +20,7 @@ constexpr int NSLOT = 32;         // reduced sums per chain (4 + NNP <= 32)
 constexpr int MPW = 32;           // model-parameter words per chain (theta[3], pad, yGP[NNP])
 constexpr int POOL_VECS = 2;      // vectors per proposal-pool slot in HBM (q, grad)
 constexpr int KMAX = 24;          // max GP control points (K^-1 tile in LDS)
-constexpr int NSTAMP = 72;        // diagnostic stamps per tile (FITOCT_STAMPS)
+constexpr int NSTAMP = 84;        // diagnostic stamps per tile (FITOCT_STAMPS)
 
 // how a tile evaluates the GP modulation dL = B yGP and its adjoint B^T h.
 // With BPT > 0 a lane's bins stay in VGPRs for the whole run, with BPT == 0 the

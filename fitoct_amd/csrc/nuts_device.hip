@@ -2718,6 +2718,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     Bins<R, BPT, NNP, MODE> bins;
     bins.load(P, tid);
     int zero_done[GMAX] = {0, 0, 0, 0};
+    // profiling build: tile occupancy -- real time and sweeps by the tile's live chains
+    // (0..4) at each ring entry (wave 0; the tail of a launch is its thinned-out tiles)
+    long long occ_t[GMAX + 1] = {0, 0, 0, 0, 0}, occ_n[GMAX + 1] = {0, 0, 0, 0, 0};
+    long long occ_last = kProfile ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+    int occ_k = GMAX;
     for (unsigned h = 0;; ++h) {
       unsigned long long e;
       bool stop = false;
@@ -2740,6 +2745,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       }
       if (stop) break;
       const int c = (int)(e & 0xFF);
+      if (kProfile && wave == 0 && P.stamps != nullptr) {
+        const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+        occ_t[occ_k] += now - occ_last;   // the interval since the last entry, at its count
+        occ_last = now;
+        occ_k = min(max(lds_load(&live_chains), 0), GMAX);
+        ++occ_n[occ_k];
+      }
       const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
       const long long s0w = wstamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
       if (kProfile && lane == 0) {   // sweep start spread over the 8 waves
@@ -2760,6 +2772,14 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       if (stamp) {
         t_busy += (long long)__builtin_amdgcn_s_memtime() - s0;
         ++n_items;
+      }
+    }
+    if (kProfile && wave == 0 && lane == 0 && P.stamps != nullptr) {
+      AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)blockIdx.x * NSTAMP;
+      occ_t[occ_k] += (long long)__builtin_amdgcn_s_memrealtime() - occ_last;
+      for (int k = 0; k <= GMAX; ++k) {
+        o[72 + k] = occ_t[k];
+        o[77 + k] = occ_n[k];
       }
     }
   } else {           // ------------------------- NUTS waves
