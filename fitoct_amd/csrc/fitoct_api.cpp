@@ -776,8 +776,8 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
     k.mig_tiles = T;
     k.mig_img_words = words;
   }
-  // Speculative leaves (nuts_device.hip leaf_spec).  A tile of one chain always
-  // speculates, with a spare NUTS wave helping (config 2 +4 %).  A tile of several chains
+  // Speculative leaves (nuts_device.hip leaf_spec).  A tile of one (two) chain(s) always
+  // speculates, with a spare NUTS wave helping each chain (config 2 +4 %).  A tile of several chains
   // has no spare wave: while it hosts 4 live chains the sweep hides the sampler's latency
   // and speculation only adds work, so a migrating chain speculates only once its tile has
   // thinned out to <= kSpecLiveMigrating chains (the launch's tail, config 3 +2 %).  Draws
@@ -785,7 +785,9 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   // always), FITOCT_SPEC=1 is FITOCT_SPEC_LIVE=GMAX (tests), FITOCT_NO_SPEC=1 builds the
   // plain sampler.
   {
-    int live = k.G == 1 ? 1 : pl->mig_bytes > 0 ? kSpecLiveMigrating : 0;
+    // (tiles of two chains without migration -- a batch of 257..512 chains, config 5's
+    // per-GPU share at 2 GPUs -- have a spare NUTS wave per chain too: deep speculation)
+    int live = pl->mig_bytes > 0 ? kSpecLiveMigrating : k.G <= 2 ? 1 : 0;
     if (const char* fs = getenv("FITOCT_SPEC")) live = atoi(fs) != 0 ? GMAX : live;
     if (const char* fl = getenv("FITOCT_SPEC_LIVE")) live = atoi(fl);
     if (getenv("FITOCT_NO_SPEC") != nullptr) live = 0;

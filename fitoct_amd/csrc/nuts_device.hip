@@ -814,11 +814,11 @@ struct Lds {
     return (int)sizeof(ChainScalars) +
            (NVEC * VLEN + NSLOT + NAUX + max_depth * NLVL * VLEN + max_depth * WAVE) * 8;
   }
-  // tiles of one chain (deep speculation): the booked leaf's q, end-updated p, g, lp and
-  // sum r^2, handed from the chain's wave to the helper wave that books it
+  // tiles of one or two chains (deep speculation): per chain, the booked leaf's q,
+  // end-updated p, g, lp and sum r^2, handed from the chain's wave to its helper wave
   static constexpr int HX_BYTES = ((3 * VLEN + 2) * 8 + 15) / 16 * 16;
   static __host__ __device__ constexpr int bytes(int G, int max_depth) {
-    return head_bytes(G) + G * chain_bytes(max_depth) + (G == 1 ? HX_BYTES : 0);
+    return head_bytes(G) + G * chain_bytes(max_depth) + (G <= 2 ? G * HX_BYTES : 0);
   }
   AS_LDS char* base;
   int G, cb;
@@ -834,7 +834,11 @@ struct Lds {
   __device__ AS_LDS double* sums(int c) const { return vecs(c) + NVEC * VLEN; }
   __device__ AS_LDS double* aux(int c) const { return sums(c) + NSLOT; }
   __device__ AS_LDS double* lvls(int c) const { return aux(c) + NAUX; }
-  __device__ AS_LDS double* hx() const { return (AS_LDS double*)(base + head_bytes(G) + G * cb); }
+  // chain c's hand-off block (G <= 2); hx(0) is also where a two-ended tile's (G = 3
+  // areas) ring extension starts
+  __device__ AS_LDS double* hx(int c = 0) const {
+    return (AS_LDS double*)(base + head_bytes(G) + G * cb + c * HX_BYTES);
+  }
 };
 
 // The likelihood sweep of chains [cb, ce) of the tile (gradient waves only).
@@ -999,7 +1003,7 @@ struct Chain {
   // wave), else while the tile hosts <= P.spec_live live chains (the tail of a launch, when
   // the sweep no longer hides the sampler's latency; this wave then does the helper's part)
   static constexpr bool spec = SPEC;
-  bool helped;   // ... with a helper wave (tiles of one chain, no migration)
+  bool helped;   // ... with a helper wave (tiles of one or two chains, no migration)
   const AS_LDS int* live = nullptr;   // the tile's live-chain count (kernel-maintained)
   // a speculated leaf's values, kept from leaf_spec to act_spec_book (across the hand-off)
   // (the metric and the next subtree's start are re-read from LDS.)  The migrating
@@ -1043,9 +1047,10 @@ struct Chain {
         part(L.part()), Kinv(L.kinv()), bv(L.bv()),
         lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
     gid = Pr().chain_offset + lc;
-    helped = SPEC && !MIG && nct_ == 1;
+    // tiles of G <= 2 chains: NUTS wave G + c helps chain slot c (tile of one chain: wave 1)
+    helped = SPEC && !MIG && P_.G <= 2;
     deep = FITOCT_DEEP_SPEC && helped;
-    HX = L.hx();
+    HX = L.hx(L.G <= 2 ? slot_ : 0);   // (two-ended: L.G = 3, one ring extension)
     bidi = kTwoEnded && deep && P_.bidi != 0;
     if (bidi) {
       pvb[0] = L.vecs(1);
@@ -1880,7 +1885,7 @@ struct Chain {
   // coordinates (depth, leaf, direction, step) in Sp advanced for the next leaf exactly as
   // act_spec_book advances them -- the chain's wave reads them only after waiting for this
   // booking.  Same operations on the same values as the plain path: same draws.
-  __device__ int deep_book() {
+  __device__ __forceinline__ int deep_book() {
     V q, pe, g;
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
@@ -1891,7 +1896,7 @@ struct Chain {
     return book_leaf(q, pe, g, HX[3 * VLEN], HX[3 * VLEN + 1]);
   }
   // ... of a leaf given by value (deep_book: from HX; bidi_book: from a producer's ring)
-  __device__ int book_leaf(const V& q, const V& pe, const V& g, const double lp, const double s2) {
+  __device__ __forceinline__ int book_leaf(const V& q, const V& pe, const V& g, const double lp, const double s2) {
     const int d = uni(Sp->depth), j = uni(Sp->leaf);
     const uint32_t t = (uint32_t)uni(Sp->t);
     tree_uniforms(d, j, t);
@@ -2487,7 +2492,7 @@ struct Chain {
   }
 
   // run actions until the chain yields a position to the gradient waves (or finishes)
-  __device__ int run(int a) {
+  __device__ __forceinline__ int run(int a) {
     for (;;) {
       FITOCT_MARK(dispatch);
       a = uni(a);
@@ -2660,12 +2665,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   __shared__ int q_reserve, n_active, grad_cnt[GMAX];
   __shared__ long long done_t[GMAX];   // profiling build: when the 8th wave finished chain c
   __shared__ long long start_min[GMAX], start_max[GMAX];
-  // speculative leaves (P.spec, one chain per tile): the chain's NUTS wave posts a
-  // request {depth, leaf, iteration} for the prior part of a speculated position; the
-  // helper wave (slot 1) runs it and publishes the request number it finished
-  __shared__ int help_req, help_done, help_wdone, help_arg[3], help_res;
+  // speculative leaves (P.spec, tiles of one or two chains): chain slot c's NUTS wave posts
+  // a request for the bookkeeping of its leaf (deep: the leaf in HX[c]) or the prior part of
+  // a speculated position; its helper wave (NUTS wave G + c) runs it and publishes the
+  // request number it finished
+  __shared__ int help_req[2], help_done[2], help_wdone[2], help_arg[2][3], help_res[2];
   const bool spec = SPEC;
-  const bool helped = SPEC && !MIG && nct == 1;   // a spare NUTS wave helps the tile's one chain
+  const bool helped = SPEC && !MIG && P.G <= 2;   // spare NUTS waves help the tile's chains
   const bool bidi = Chain<PPL, NNP, FAM, MIG, SPEC>::kTwoEnded && helped &&
                    P.bidi != 0;   // ... and two producer waves
   __shared__ int live_chains;   // chains the tile hosts (speculation policy, Chain::live)
@@ -2675,10 +2681,12 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     q_reserve = 0;
     n_active = nct;
     live_chains = nct;
-    help_req = 0;
-    help_done = 0;
-    help_wdone = 0;
-    help_res = 0;
+  }
+  if (tid < 2) {
+    help_req[tid] = 0;
+    help_done[tid] = 0;
+    help_wdone[tid] = 0;
+    help_res[tid] = 0;
   }
   if (tid < GMAX) {
     grad_cnt[tid] = 0;
@@ -2969,14 +2977,15 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       wave_fence();
       if (lane == 0) atomicAdd(&bd[BD_EXIT], 1);
     }
-    if (helped && !bidi && c == 1) {   // the helper wave of slot 0's chain
+    if (helped && !bidi && c >= P.G && c - P.G < nct) {   // the helper wave of chain slot c - G
       if (FITOCT_HELPER_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_HELPER_PRIO);
       using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
-      Ch ch(P, L, 0, c0, lane, nct);
+      const int hs = c - P.G;
+      Ch ch(P, L, hs, c0 + hs, lane, nct);
       int seen = 0;
       Patience w;
       for (;;) {
-        const int r = lds_load(&help_req);
+        const int r = lds_load(&help_req[hs]);
         if (r < 0) break;                       // the chain has finished
         if (r == seen) {
           // the chain releases its helper when it finishes (help_req = -1), however long
@@ -2993,19 +3002,19 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           const int res = ch.deep_book();
           wave_fence();
           if (lane == 0) {
-            __atomic_store_n(&help_res, res, __ATOMIC_RELAXED);
+            __atomic_store_n(&help_res[hs], res, __ATOMIC_RELAXED);
             wave_fence();
-            __atomic_store_n(&help_done, seen, __ATOMIC_RELAXED);
+            __atomic_store_n(&help_done[hs], seen, __ATOMIC_RELAXED);
           }
           continue;
         }
         ch.spec_weight();   // first what the chain's bookkeeping waits for
         wave_fence();
-        if (lane == 0) __atomic_store_n(&help_wdone, seen, __ATOMIC_RELAXED);
-        ch.prior_and_uniforms(true, lds_load(&help_arg[0]), lds_load(&help_arg[1]),
-                              (uint32_t)lds_load(&help_arg[2]));
+        if (lane == 0) __atomic_store_n(&help_wdone[hs], seen, __ATOMIC_RELAXED);
+        ch.prior_and_uniforms(true, lds_load(&help_arg[hs][0]), lds_load(&help_arg[hs][1]),
+                              (uint32_t)lds_load(&help_arg[hs][2]));
         wave_fence();
-        if (lane == 0) __atomic_store_n(&help_done, seen, __ATOMIC_RELAXED);
+        if (lane == 0) __atomic_store_n(&help_done[hs], seen, __ATOMIC_RELAXED);
       }
     }
     if (c < (mig ? P.G : nct)) {
@@ -3065,20 +3074,20 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
                              __ATOMIC_RELAXED);
             if (ch.deep) {
               wave_fence();   // the hand-off (HX) lands before the request number
-              __atomic_store_n(&help_req, hreq + 1, __ATOMIC_RELAXED);
+              __atomic_store_n(&help_req[c], hreq + 1, __ATOMIC_RELAXED);
             } else if (helped) {
-              help_arg[0] = ch.k_dn;
-              help_arg[1] = ch.k_jn;
-              help_arg[2] = (int)ch.k_t;
+              help_arg[c][0] = ch.k_dn;
+              help_arg[c][1] = ch.k_jn;
+              help_arg[c][2] = (int)ch.k_t;
               wave_fence();   // the arguments land before the request number
-              __atomic_store_n(&help_req, hreq + 1, __ATOMIC_RELAXED);
+              __atomic_store_n(&help_req[c], hreq + 1, __ATOMIC_RELAXED);
             }
           }
           if (stamp) t_enq = (long long)__builtin_amdgcn_s_memtime();
           if (ch.deep) {   // the helper books the leaf; this wave computes the next prior part
             ++hreq;
-            ch.book_done = (volatile AS_LDS int*)&help_done;
-            ch.book_res = (volatile AS_LDS int*)&help_res;
+            ch.book_done = (volatile AS_LDS int*)&help_done[c];
+            ch.book_res = (volatile AS_LDS int*)&help_res[c];
             ch.book_want = hreq;
             ++epoch;
             a = Ch::A_PRIOR;
@@ -3087,7 +3096,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           }
           if (helped) {
             ++hreq;
-            ch.help_wdone = (volatile AS_LDS int*)&help_wdone;
+            ch.help_wdone = (volatile AS_LDS int*)&help_wdone[c];
             ch.help_want = hreq;
           }
           ++epoch;
@@ -3099,7 +3108,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           Patience w;
           const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
           if (stamp) t_busy += w0 - s0;
-          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch) || lds_load(&help_done) < hreq) {
+          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch) || lds_load(&help_done[c]) < hreq) {
             if (w.expired(LEAF_WAIT_TICKS)) {
               late = true;
               break;
@@ -3183,7 +3192,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
                       (unsigned long long)__builtin_amdgcn_s_memrealtime());
             atomicAdd(&chains_done_here, 1);
           }
-          if (helped && lane == 0) __atomic_store_n(&help_req, -1, __ATOMIC_RELAXED);   // release the helper
+          if (helped && lane == 0) __atomic_store_n(&help_req[c], -1, __ATOMIC_RELAXED);   // release the helper
           if (bidi) {   // release the producers and the helper; the producers drain their sweeps
             if (lane == 0) __atomic_store_n(&bd[BD_GEN], -1, __ATOMIC_RELAXED);
             Patience w;

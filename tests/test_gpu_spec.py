@@ -215,3 +215,40 @@ def test_batch_of_one_chain_tiles_two_ended_bitwise():
                 os.environ[k] = v
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x.draws, y.draws)
+
+
+@pytest.mark.parametrize("files,chains,env", [(80, 4, {}), (75, 4, {}),
+                                              (1, 301, {"FITOCT_NO_MIGRATE": "1"})])
+def test_two_chain_tiles_deep_speculation_bitwise(files, chains, env):
+    """Tiles of two chains without migration (257..512 chains: config 5's per-GPU share at 2
+    GPUs, 128 files x 4 chains) give each chain a spare NUTS wave as its helper (wave 2 + c
+    books chain c's leaves while chain c's wave completes the next gradient and stages the
+    one after): same draws, step sizes and leapfrog counts as the plain sampler, including
+    a last tile that hosts one chain (301 chains)."""
+    from fitoct_amd import Batch
+    probs = [_prob("normal", 481, 15, seed=200 + f) for f in range(files)]
+    cfg = SamplerConfig(chains=chains, warmup=40, samples=30, seed=13)
+    outs = {}
+    for spec in (True, False):
+        old = {k: os.environ.get(k) for k in ("FITOCT_NO_SPEC", "FITOCT_SPEC", *env)}
+        try:
+            for k in old:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            if not spec:
+                os.environ["FITOCT_NO_SPEC"] = "1"
+            with Batch(probs, cfg) as b:
+                b.run()
+                outs[spec] = (b.info, [b.download(p) for p in range(files)])
+        finally:
+            for k, v in old.items():
+                os.environ.pop(k, None)
+                if v is not None:
+                    os.environ[k] = v
+    (ia, a), (ib, b) = outs[True], outs[False]
+    assert ia["chains_per_tile"] == 2 and ia["sampler"] == 2 and ib["sampler"] == 0
+    assert ia["lds_bytes"] <= 160 * 1024
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x.draws, y.draws)
+        np.testing.assert_array_equal(x.stepsize, y.stepsize)
+        assert x.total_leapfrogs == y.total_leapfrogs
