@@ -63,7 +63,7 @@ class Result(C.Structure):
         ("inv_metric", _dp), ("last_q", _dp), ("chain_status", _ip),
         ("n_cols", C.c_int32), ("iters_saved", C.c_int32), ("dim", C.c_int32),
         ("migrations", C.c_int32), ("total_leapfrogs", C.c_int64), ("kernel_ms", C.c_double),
-        ("wall_ms", C.c_double),
+        ("wall_ms", C.c_double), ("two_ended_transitions", C.c_int64),
     ]
 
 

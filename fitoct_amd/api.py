@@ -196,6 +196,7 @@ class SampleOutput:
     chain_offset: int = 0
     migrations: int = 0        # chains handed between tiles (work balance)
     cfg: object = None         # the SamplerConfig of the run (Stan-CSV header)
+    two_ended_transitions: int = 0   # transitions grown at both ends at once (no effect on draws)
 
 
 class Plan:
@@ -298,7 +299,8 @@ class Plan:
         return SampleOutput(draws, self.prob.column_names(),
                             self.cfg.warmup if self.cfg.save_warmup else 0, eps, minv, lq,
                             int(r.total_leapfrogs), float(r.kernel_ms), 0.0,
-                            self.cfg.chain_offset, int(r.migrations), self.cfg)
+                            self.cfg.chain_offset, int(r.migrations), self.cfg,
+                            int(r.two_ended_transitions))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -366,7 +368,8 @@ class Batch:
                             int(r.total_leapfrogs), float(r.kernel_ms), 0.0,
                             self.cfg.chain_offset + problem * C_, 0,
                             dataclasses.replace(self.cfg,
-                                                chain_offset=self.cfg.chain_offset + problem * C_))
+                                                chain_offset=self.cfg.chain_offset + problem * C_),
+                            int(r.two_ended_transitions))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -726,7 +726,8 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
     HIP_TRY(hipMalloc(&pl->d_stack, sizeof(double) * (size_t)C * (cfg->max_treedepth + 1) * POOL_VECS * vlen));
     HIP_TRY(hipMalloc(&pl->d_fin, sizeof(double) * (size_t)C * (1 + 2 * D)));
     HIP_TRY(hipMalloc(&pl->d_status, sizeof(int) * C));
-    HIP_TRY(hipMalloc(&pl->d_leap, sizeof(long long) * C));
+    // [chains] leapfrogs per chain, then the two-ended transition count of the launch
+    HIP_TRY(hipMalloc(&pl->d_leap, sizeof(long long) * (C + 1)));
     HIP_TRY(hipEventCreate(&pl->ev0));
     HIP_TRY(hipEventCreate(&pl->ev1));
     return FITOCT_OK;
@@ -739,6 +740,7 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   k.fin_q = pl->d_fin + C + (size_t)C * D;
   k.chain_status = pl->d_status;
   k.leapfrogs = pl->d_leap;
+  k.bidi_count = (unsigned long long*)(pl->d_leap + C);
   if (g_chains == 0) {   // progress / cancellation (fitoct_plan_poll / _cancel); batch: off
     auto prog_setup = [&]() -> int {
       HIP_TRY(hipHostMalloc((void**)&pl->h_prog, sizeof(int) * C,
@@ -816,6 +818,22 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
       k.bidi_rba = std::min(ra, rb);
       k.bidi_rec = rec;
       pl->lds = base + 2 * (rb - k.bidi_rba) * rec * 8;
+    }
+  }
+  // Two-ended trajectories in the tail of a migrating launch (nuts_device.hip receive_chain):
+  // the rings live in the producers' own tree-level areas (no LDS added).  Same draws bit
+  // for bit.  FITOCT_NO_TAIL_BIDI=1: off; FITOCT_TAIL_LEFT=n: start at n unfinished chains
+  // (default: one per tile).
+  k.tail_bidi = 0;
+  if (pl->mig_bytes > 0 && k.spec && getenv("FITOCT_NO_TAIL_BIDI") == nullptr) {
+    const int rec = (3 * D + 2 + 1) / 2 * 2;
+    const int ra = std::min(256, lvl_doubles(pl->ppl, k.max_depth) / rec);
+    if (ra >= 4) {
+      k.tail_bidi = 1;
+      k.bidi_rb = k.bidi_rba = ra;
+      k.bidi_rec = rec;
+      k.tail_left = pl->tiles;
+      if (const char* e = getenv("FITOCT_TAIL_LEFT")) k.tail_left = std::max(0, atoi(e));
     }
   }
   *out = guard.release();
@@ -897,6 +915,7 @@ int32_t fitoct_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
     KParams k = pl->kp;
     k.draws = dst;
     HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * k.chains, st));
+    HIP_TRY(hipMemsetAsync(k.bidi_count, 0, sizeof(long long), st));
     if (pl->d_mig) HIP_TRY(hipMemsetAsync(pl->d_mig, 0, pl->mig_bytes, st));
     const bool want_stamps = getenv("FITOCT_STAMPS") != nullptr;   // diagnostic only
     if (want_stamps) {
@@ -1112,6 +1131,9 @@ int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
     long long tot = 0;
     for (long long v : lf) tot += v;
     res->total_leapfrogs = tot;
+    long long nb = 0;
+    HIP_TRY(hipMemcpy(&nb, k.bidi_count, sizeof(long long), hipMemcpyDeviceToHost));
+    res->two_ended_transitions = nb;
     if (bad >= 0)
       return fail(st[bad], "chain " + std::to_string(k.chain_offset + bad) + " failed with status " +
                                std::to_string(st[bad]));
@@ -1320,6 +1342,7 @@ int fitoct::batch_run_single(fitoct_batch* b, void* d_draws, void* stream) {
       kp[p].cancel = b->d_cancel;
       pl->last_draws = kp[p].draws;
       HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * pl->kp.chains, st));
+      HIP_TRY(hipMemsetAsync(pl->kp.bidi_count, 0, sizeof(long long), st));
     }
     HIP_TRY(hipMemcpyAsync(b->d_kp, kp.data(), sizeof(KParams) * P, hipMemcpyHostToDevice, st));
     const fitoct_plan* p0 = b->plans[0];

@@ -121,6 +121,13 @@ struct KParams {
   int bidi_rec;             // doubles per record: q, end-updated p, g (D each), lp, sum r^2
   int bidi_rba;             // records of each ring in its producer's (unused) tree-level area;
                             // the other bidi_rb - bidi_rba behind the chain areas
+  // ---- two-ended trajectories in a migrating launch's tail (0: off) ----
+  // once at most tail_left chains of the launch are unfinished, a chain alone in its tile
+  // recruits two of the tile's idle receivers as producers and books its trees itself;
+  // rings of bidi_rb = bidi_rba records in the producers' tree-level areas
+  int tail_bidi;
+  int tail_left;
+  unsigned long long* bidi_count;   // two-ended transitions of the launch (fitoct_result)
 };
 
 }  // namespace fitoct

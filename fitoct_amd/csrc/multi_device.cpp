@@ -406,9 +406,11 @@ int group_plan_download(fitoct_plan* pl, fitoct_result* res) {
   res->kernel_ms = pl->kernel_ms;
   res->migrations = 0;
   res->total_leapfrogs = 0;
+  res->two_ended_transitions = 0;
   for (const fitoct_result& s : sub) {
     res->migrations += s.migrations;
     res->total_leapfrogs += s.total_leapfrogs;
+    res->two_ended_transitions += s.two_ended_transitions;
   }
   return rc;
 }

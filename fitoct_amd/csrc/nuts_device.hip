@@ -162,8 +162,18 @@ static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
 // (1..BD_GEN_MASK, -1: the chain has finished); BD_PROD + s: stream s's published leaves as
 // (gen << 16) | count; BD_CONS + s: leaves of stream s the helper has booked; BD_END: the
 // transition whose tree the helper has ended; BD_EXIT: producers that have left
-enum BdWord : int { BD_GEN = 0, BD_PROD = 1, BD_CONS = 3, BD_END = 5, BD_EXIT = 6, BD_N = 8 };
+// TW_*: who grows the ends -- the producers' NUTS slots (TW_SLOT, TW_SLOT + 1; a tile of
+// one chain: 1, 2), the chain's slot and index (TW_CHAIN, TW_LC; written by bidi_begin);
+// migrating tiles recruit producers at run time (TW_CLAIM: role bits claimed, TW_JOIN:
+// producers in place; see receive_chain)
+enum BdWord : int {
+  BD_GEN = 0, BD_PROD = 1, BD_CONS = 3, BD_END = 5, BD_EXIT = 6,
+  TW_CLAIM = 7, TW_JOIN = 8, TW_SLOT = 9, TW_CHAIN = 11, TW_LC = 12, BD_N = 16
+};
 constexpr int BD_GEN_MASK = (1 << 15) - 1;
+// BD_GEN | BD_ENDED: a migrating tile's chain has booked transition BD_GEN's tree to its end
+// (its producers stop, and wait for the next transition or the launch's end)
+constexpr int BD_ENDED = 1 << 20;
 // the chain's wave while the producers and the helper grow a tree: its priority (-1: the NUTS
 // priority) and poll interval (A/B knobs)
 #ifndef FITOCT_BIDI_IDLE_PRIO
@@ -991,7 +1001,7 @@ struct Chain {
   // this lane's row of K^-1 (lanes < NNP) held in VGPRs for the two K^-1 matvecs
   // of every leaf (write_mp, finish_grad): same arithmetic, no LDS reads on the
   // NUTS wave's critical path (configs 2 / 5 +2 %).  Not at NNP = 24 (it would spill).
-  static constexpr bool KROW = NNP <= 16;
+  static constexpr bool KROW = NNP <= 16 && !MIG;
   // fexp's Horner steps as three-VGPR FMAs (fma_v) in the non-migrating samplers: bitwise
   // the same, configs 2 / 5 +2 / +0.6 %.  The migrating samplers then spill a VGPR (the
   // headline horseshoe one loses 2.2 %, profiles/r03_ab_fmav.txt): they keep the compiler's form
@@ -1030,14 +1040,11 @@ struct Chain {
   int book_want = 0;
   // two-ended trajectories (P.bidi, deep tiles): the producer waves' chain areas (slots 1, 2:
   // backward, forward) and the tile's hand-off words BD_*
-  // (compiled only where it can run: a migrating tile never has the spare waves, and the
-  // two-ended code in its kernel costs the headline instantiation a spilled VGPR)
-  static constexpr bool kTwoEnded = SPEC && !MIG && FITOCT_DEEP_SPEC;
+  // Compiled where it can run: tiles of one chain (deep speculation, spare waves from the
+  // start), and migrating tiles in the launch's tail (a chain alone in its tile, with two
+  // idle receivers recruited as producers: kernel and receive_chain, P.tail_bidi)
+  static constexpr bool kTwoEnded = SPEC && FITOCT_DEEP_SPEC;
   bool bidi = false;
-  AS_LDS double* pvb[2] = {nullptr, nullptr};
-  AS_LDS ChainScalars* psp[2] = {nullptr, nullptr};
-  AS_LDS double* plv0 = nullptr;   // (two scalars: a runtime-indexed member array would put
-  AS_LDS double* plv1 = nullptr;   //  the whole chain object in scratch)
   volatile AS_LDS int* bd = nullptr;
   RngKey key;
 
@@ -1051,15 +1058,7 @@ struct Chain {
     helped = SPEC && !MIG && P_.G <= 2;
     deep = FITOCT_DEEP_SPEC && helped;
     HX = L.hx(L.G <= 2 ? slot_ : 0);   // (two-ended: L.G = 3, one ring extension)
-    bidi = kTwoEnded && deep && P_.bidi != 0;
-    if (bidi) {
-      pvb[0] = L.vecs(1);
-      pvb[1] = L.vecs(2);
-      psp[0] = &L.cs(1);
-      psp[1] = &L.cs(2);
-      plv0 = L.lvls(1);
-      plv1 = L.lvls(2);
-    }
+    bidi = kTwoEnded && !MIG && deep && P_.bidi != 0;
     key = make_key(Pr().seed, (uint32_t)gid);
     if constexpr (KROW) {
       const int r = lane < NNP ? lane : 0;
@@ -1073,6 +1072,22 @@ struct Chain {
   }
 
   __device__ __forceinline__ KPc& Pr() const { return *pp; }
+  // two-ended trajectories: producer k's chain area (NUTS slot bd[TW_SLOT + k] of this
+  // tile: the chain areas are consecutive, chain_bytes apart), its scalars, vectors and
+  // tree-level area (where the first bidi_rba records of its ring sit)
+  __device__ __forceinline__ AS_LDS char* parea(int k) const {
+    const int sl = __builtin_amdgcn_readfirstlane(bd[TW_SLOT + k]);
+    return (AS_LDS char*)Sp + (sl - slot) * Lds<PPL>::chain_bytes(Pr().max_depth);
+  }
+  __device__ __forceinline__ AS_LDS ChainScalars* psp(int k) const {
+    return (AS_LDS ChainScalars*)parea(k);
+  }
+  __device__ __forceinline__ AS_LDS double* pvb(int k) const {
+    return (AS_LDS double*)(parea(k) + sizeof(ChainScalars));
+  }
+  __device__ __forceinline__ AS_LDS double* plv(int k) const {
+    return pvb(k) + NVEC * VLEN + NSLOT + NAUX;
+  }
   __device__ __forceinline__ int idx(int s) const { return s * WAVE + lane; }
   __device__ __forceinline__ bool ok(int s) const { return idx(s) < Pr().D; }
   __device__ __forceinline__ AS_LDS double* vec(int v) const { return Vb + v * VLEN; }
@@ -1730,6 +1745,7 @@ struct Chain {
     FITOCT_MARK(act_begin_subtree);
     if constexpr (kTwoEnded) {
       if (bidi) return bidi_begin();   // reached at depth 0 only: the helper books from there on
+      if (MIG && tail_ready()) return bidi_begin();   // (the chain's own wave books, kernel)
     }
     const int d = uni(Sp->depth);
     const double u = uniform(key, (uint32_t)uni(Sp->t), TAG_DIR, (uint32_t)d, 0u);
@@ -1953,8 +1969,46 @@ struct Chain {
   // a producer never uses)
   __device__ AS_LDS double* brec(int s, int n) const {
     const int rb = Pr().bidi_rb, ra = Pr().bidi_rba, m = n % rb;
-    return m < ra ? (s ? plv1 : plv0) + m * Pr().bidi_rec
+    return m < ra ? plv(s) + m * Pr().bidi_rec
                   : HX + (s * (rb - ra) + (m - ra)) * Pr().bidi_rec;
+  }
+  // a migrating tile's chain, at the start of a transition (depth 0): two-ended when it is
+  // the tile's only live chain and two idle receivers of the tile have become producers
+  __device__ __forceinline__ bool tail_ready() const {
+    return Pr().tail_bidi != 0 && uni(Sp->depth) == 0 && uni(bd[TW_JOIN]) >= 2 &&
+           uni(__atomic_load_n(live, __ATOMIC_RELAXED)) == 1;
+  }
+  // Book every leaf of transition g in Stan's tree order from the producers' rings: the
+  // helper wave of a tile of one chain, or a migrating tile's chain itself.  LB_END, with
+  // the status ERR_TIMEOUT if a producer's record never came (a fault)
+  __device__ int bidi_book_tree(const int g) {
+    int cons0 = 0, cons1 = 0;
+    for (;;) {
+      const int s = uni(Sp->dir);   // the subtree being booked grows this end
+      const int n = s ? cons1 : cons0;
+      bool lost = false;
+      Patience wl;   // one producer leaf: its throttle never holds back the leaf booked next
+      for (;;) {     // leaf n of stream s published for this transition
+        const int w = bd[BD_PROD + s];
+        if ((w >> 16) == g && (w & 0xFFFF) > n) break;
+        if (bd[BD_GEN] != g || wl.expired(LEAF_WAIT_TICKS)) {   // never, short of a fault
+          lost = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (lost) {
+        Sp->status = ERR_TIMEOUT;
+        return LB_END;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the record after its count
+      const int r = bidi_book(s, n);
+      if (s) ++cons1;
+      else ++cons0;
+      wave_fence();
+      if (lane == 0) bd[BD_CONS + s] = n + 1;
+      if (r == LB_END) return LB_END;
+    }
   }
   // the chain's wave, at depth 0 of a transition: act_begin_subtree's bookkeeping, the start
   // to both producers' slots, then the transition's number (BD_GEN) releases them
@@ -1969,26 +2023,33 @@ struct Chain {
     Sp->lf_e = dir ? Sp->eps_used : -Sp->eps_used;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
+      AS_LDS double* const pv = pvb(k);
+      AS_LDS ChainScalars* const ps = psp(k);
 #pragma unroll
       for (int s = 0; s < PPL; ++s) {
-        pvb[k][V_E0_Q * VLEN + idx(s)] = q.a[s];
-        pvb[k][V_E0_P * VLEN + idx(s)] = p.a[s];
-        pvb[k][V_E0_G * VLEN + idx(s)] = g.a[s];
-        pvb[k][V_MINV * VLEN + idx(s)] = minv.a[s];
+        pv[V_E0_Q * VLEN + idx(s)] = q.a[s];
+        pv[V_E0_P * VLEN + idx(s)] = p.a[s];
+        pv[V_E0_G * VLEN + idx(s)] = g.a[s];
+        pv[V_MINV * VLEN + idx(s)] = minv.a[s];
       }
       if (lane == 0) {
-        psp[k]->eps_used = Sp->eps_used;
-        psp[k]->t = (int)t;
-        psp[k]->end_lp[0] = Sp->end_lp[0];
-        psp[k]->end_s2[0] = Sp->end_s2[0];
+        ps->eps_used = Sp->eps_used;
+        ps->t = (int)t;
+        ps->end_lp[0] = Sp->end_lp[0];
+        ps->end_s2[0] = Sp->end_s2[0];
       }
     }
     if (lane == 0) {
       bd[BD_CONS] = 0;
       bd[BD_CONS + 1] = 0;
+      bd[TW_CHAIN] = slot;   // the producers read the booked depth and the key from these
+      bd[TW_LC] = lc;
     }
     wave_fence();   // every store above lands before the transition's number
-    if (lane == 0) bd[BD_GEN] = (bd[BD_GEN] & BD_GEN_MASK) % BD_GEN_MASK + 1;
+    if (lane == 0) {
+      bd[BD_GEN] = (bd[BD_GEN] & BD_GEN_MASK) % BD_GEN_MASK + 1;
+      atomicAdd(Pr().bidi_count, 1ULL);
+    }
     return A_BIDI_TREE;
   }
   // the helper: book leaf n of stream s (published: its record is in the ring).  Lanes past D
@@ -2588,8 +2649,14 @@ constexpr int RINGN = 16;                 // hand-off ring: >= 2 * GMAX entries
 // Receivers wait only once every tile of the launch has started: then no tile
 // is waiting for a CU, so waiting cannot starve one.  An idle wait longer than
 // MIG_WAIT_TICKS withdraws the post (if no donor claimed it meanwhile).
+// The launch's tail (P.tail_bidi; at most P.tail_left chains left unfinished): a receiver
+// whose tile hosts exactly one live chain withdraws its post and becomes one of that chain's
+// two producers of two-ended trajectories (returns -2 - end; one claim bit per end in
+// TW_CLAIM, the slot in TW_SLOT + end, TW_JOIN counts producers in place).  A tile whose
+// claims are taken keeps its other free slots posted.
 template <int PPL>
-__device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane) {
+__device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane, volatile AS_LDS int* bd,
+                             const AS_LDS int* live) {
   const MigView M(P.mig, P.mig_tiles);
   const int me = blockIdx.x;
   if (__builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_STARTED])) < P.mig_tiles) return -1;
@@ -2606,7 +2673,30 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane) {
   for (;;) {
     m = __builtin_amdgcn_readfirstlane(g_load(box));
     if (m != 0) break;
-    if (__builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_DONE])) >= P.chains) return -1;
+    const int done = __builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_DONE]));
+    if (done >= P.chains) return -1;
+    if (P.tail_bidi && P.chains - done <= P.tail_left &&
+        __builtin_amdgcn_readfirstlane(*(volatile const AS_LDS int*)live) == 1 &&
+        __builtin_amdgcn_readfirstlane(bd[TW_CLAIM]) != 3) {
+      int r = -1;
+      if (lane == 0) {
+        for (int k = 0; k < 2 && r < 0; ++k)
+          if (((atomicOr((int*)&bd[TW_CLAIM], 1 << k) >> k) & 1) == 0) r = k;
+        if (r >= 0) {
+          if ((g_and(&M.fmask[me], ~(1 << c)) >> c) & 1) {   // withdrawn: no migrant comes here
+            g_add(&M.hdr[MIG_WAITING], -1);
+            bd[TW_SLOT + r] = c;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            atomicAdd((int*)&bd[TW_JOIN], 1);
+          } else {   // a donor claimed this slot first: receive its chain, free the end
+            atomicAnd((int*)&bd[TW_CLAIM], ~(1 << r));
+            r = -1;
+          }
+        }
+      }
+      r = __builtin_amdgcn_readfirstlane(__shfl(r, 0));
+      if (r >= 0) return -2 - r;
+    }
     if (__builtin_amdgcn_s_memrealtime() - t0 > MIG_WAIT_TICKS) {
       int still = 0;   // withdraw the post unless a donor already claimed it
       if (lane == 0) {
@@ -2695,7 +2785,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     start_max[tid] = 0;
   }
   if (tid < RINGN) ring[tid] = ~0ULL;
-  if (tid < BD_N) bd[tid] = 0;
+  // (a tile of one chain: the producers' areas are NUTS slots 1 and 2)
+  if (tid < BD_N) bd[tid] = (tid == TW_SLOT) ? 1 : (tid == TW_SLOT + 1) ? 2 : 0;
   if (MIG && P.mig != nullptr) {   // every slot of the tile may host migrants: all NUTS waves live
     if (tid == 0) {
       const MigView M(P.mig, P.mig_tiles);
@@ -2801,82 +2892,46 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     }
     const int c = wave - NGW;
     const bool mig = MIG && P.mig != nullptr;
-    if (bidi && c == 1) {   // two-ended trajectories: book every leaf in tree order
-      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
-      Ch ch(P, L, 0, c0, lane, nct);
-      ch.bd = (volatile AS_LDS int*)bd;
-      int seen = 0;
-      for (;;) {
-        int g;
-        Patience w;   // (init and step-size searches run between transitions)
-        bool quit = false;
-        while ((g = lds_load(&bd[BD_GEN])) == seen) {   // the next transition, or the end
-          if (w.expired(MIG_WAIT_TICKS)) {
-            quit = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (quit || g < 0) break;
-        seen = g;
-        wave_fence();   // the transition's start state is read after its number
-        int cons0 = 0, cons1 = 0;
-        for (;;) {
-          const int s = ch.uni(ch.Sp->dir);   // the subtree being booked grows this end
-          const int n = s ? cons1 : cons0;
-          bool lost = false;
-          Patience wl;   // one producer leaf: its throttle never holds back the leaf booked next
-          for (;;) {   // leaf n of stream s published for this transition
-            const int w = lds_load(&bd[BD_PROD + s]);
-            if ((w >> 16) == g && (w & 0xFFFF) > n) break;
-            if (lds_load(&bd[BD_GEN]) != g || wl.expired(LEAF_WAIT_TICKS)) {   // never, short of a fault
-              lost = true;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-          int r = Ch::LB_END;
-          if (lost) {
-            ch.Sp->status = ERR_TIMEOUT;
-          } else {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the record after its count
-            r = ch.bidi_book(s, n);
-            if (s) ++cons1;
-            else ++cons0;
-            wave_fence();
-            if (lane == 0) __atomic_store_n(&bd[BD_CONS + s], n + 1, __ATOMIC_RELAXED);
-          }
-          if (r == Ch::LB_END) {
-            wave_fence();   // the booking's LDS writes land before the end is published
-            if (lane == 0) __atomic_store_n(&bd[BD_END], g, __ATOMIC_RELAXED);
-            break;
-          }
-        }
-      }
-    }
-    if (bidi && c >= 2) {   // two-ended trajectories: producer of the backward (c = 2) / forward end
-      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
-      const int s = c - 2, slot = c - 1;
+    using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
+    // Two-ended trajectories: producer of trajectory end s (0: backward, 1: forward) on NUTS
+    // slot `slot` (its chain area holds the end's state; its ring of leaf records sits in the
+    // area's tree levels and, in a tile of one chain, behind the chain areas).  For every
+    // transition g the chain starts (BD_GEN), it leapfrogs this end from the start through
+    // the doublings drawn in direction s, at most FITOCT_BIDI_LOOK doublings past the one
+    // being booked and a ring ahead of the booking, and publishes each leaf's record.
+    // `epoch`: the slot's sweeps so far (grad_cnt[slot] counts NGW per sweep).  Ends with
+    // BD_GEN < 0 (the tile's chain finished) or, in a migrating tile, with the launch.
+    auto produce = [&](const int s, const int slot, long long epoch) {
       Ch pr(P, L, slot, c0, lane, nct);
-      const AS_LDS ChainScalars& S0 = L.cs(0);   // the booked depth (the helper's)
-      long long epoch = 0;
+      pr.bd = (volatile AS_LDS int*)bd;
       int seen = 0;
       bool quit = false;
       while (!quit) {
         int g;
         {
           Patience w;
-          while ((g = lds_load(&bd[BD_GEN])) == seen) {
+          int polls = 0;
+          while ((g = lds_load(&bd[BD_GEN])) == seen || (g > 0 && (g & BD_ENDED))) {
             if (w.expired(MIG_WAIT_TICKS)) {
               quit = true;
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            if (MIG && (++polls & 255) == 0 &&
+                __builtin_amdgcn_readfirstlane(g_load(&MigView(P.mig, P.mig_tiles).hdr[MIG_DONE])) >=
+                    P.chains) {
+              quit = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(MIG ? 8 : 1);
           }
         }
         if (quit || g < 0) break;
         seen = g;
         wave_fence();
+        // the chain being grown: its key (direction draws) and its scalars (booked depth)
+        const int lcg = lds_load(&bd[TW_LC]);
+        pr.key = make_key(P.seed, (uint32_t)(P.chain_offset + lcg));
+        const AS_LDS ChainScalars& S0 = L.cs(lds_load(&bd[TW_CHAIN]));
         Vd<PPL> q = pr.ld(V_E0_Q), p = pr.ld(V_E0_P), gr = pr.ld(V_E0_G);
         const Vd<PPL> minv = pr.ld(V_MINV);
         const double eps = pr.Sp->eps_used;
@@ -2910,8 +2965,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
               break;
             }
             // the other end may grow for long (deep trees, large N).  In effect this wait
-            // ends with BD_GEN: its bound outlasts the chain wave's bound on the whole tree
-            // (MIG_WAIT_TICKS from the tree's start), after which BD_GEN changes
+            // ends with BD_GEN: its bound outlasts the bound on the whole tree (MIG_WAIT_TICKS
+            // from the tree's start), after which BD_GEN changes
             if (w.expired(2 * MIG_WAIT_TICKS)) break;
             __builtin_amdgcn_s_sleep(1);
           }
@@ -2974,6 +3029,32 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           ++n;
         }
       }
+    };
+    if (bidi && c == 1) {   // two-ended trajectories: book every leaf in tree order
+      Ch ch(P, L, 0, c0, lane, nct);
+      ch.bd = (volatile AS_LDS int*)bd;
+      int seen = 0;
+      for (;;) {
+        int g;
+        Patience w;   // (init and step-size searches run between transitions)
+        bool quit = false;
+        while ((g = lds_load(&bd[BD_GEN])) == seen) {   // the next transition, or the end
+          if (w.expired(MIG_WAIT_TICKS)) {
+            quit = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (quit || g < 0) break;
+        seen = g;
+        wave_fence();   // the transition's start state is read after its number
+        ch.bidi_book_tree(g);
+        wave_fence();   // the booking's LDS writes land before the end is published
+        if (lane == 0) __atomic_store_n(&bd[BD_END], g, __ATOMIC_RELAXED);
+      }
+    }
+    if (bidi && c >= 2) {   // two-ended trajectories: producer of the backward (c = 2) / forward end
+      produce(c - 2, c - 1, 0);
       wave_fence();
       if (lane == 0) atomicAdd(&bd[BD_EXIT], 1);
     }
@@ -3040,17 +3121,25 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if (lowp) __builtin_amdgcn_s_setprio(3);
         if (Ch::kTwoEnded && y == Ch::A_BIDI_TREE) {   // the producers and the helper grow the tree
           const int g = lds_load(&bd[BD_GEN]);
-          Patience w;
           bool late = false;
-          if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_BIDI_IDLE_PRIO);
-          while (lds_load(&bd[BD_END]) != g) {   // a whole tree
-            if (w.expired(MIG_WAIT_TICKS)) {
-              late = true;
-              break;
+          if constexpr (MIG) {   // no helper wave in a migrating tile: the chain books itself
+            ch.bidi_book_tree(g);
+          } else {
+            Patience w;
+            if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_BIDI_IDLE_PRIO);
+            while (lds_load(&bd[BD_END]) != g) {   // a whole tree
+              if (w.expired(MIG_WAIT_TICKS)) {
+                late = true;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(FITOCT_BIDI_IDLE_SLEEP);
             }
-            __builtin_amdgcn_s_sleep(FITOCT_BIDI_IDLE_SLEEP);
+            if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
           }
-          if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
+          if constexpr (MIG) {   // the producers stop growing this tree
+            wave_fence();
+            if (lane == 0) __atomic_store_n(&bd[BD_GEN], g | BD_ENDED, __ATOMIC_RELAXED);
+          }
           wave_fence();   // the helper's bookkeeping is read after the end
           // the helper's booked leaves count toward the step bound like the chain's own
           steps += ch.uni(ch.Sp->n_leapfrog);
@@ -3108,7 +3197,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           Patience w;
           const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
           if (stamp) t_busy += w0 - s0;
-          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch) || lds_load(&help_done[c]) < hreq) {
+          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch) ||
+                 (helped && lds_load(&help_done[c]) < hreq)) {
             if (w.expired(LEAF_WAIT_TICKS)) {
               late = true;
               break;
@@ -3241,7 +3331,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         }
        }
         if (!mig) break;
-        lc = receive_chain<PPL>(P, L, c, lane);
+        lc = receive_chain<PPL>(P, L, c, lane, (volatile AS_LDS int*)bd, (const AS_LDS int*)&live_chains);
+        if constexpr (Ch::kTwoEnded) {
+          if (lc <= -2) {   // recruited as a producer of the tile's lone chain (the tail)
+            produce(-2 - lc, c, epoch);
+            break;
+          }
+        }
         if (lc < 0) break;
         if (spec && lane == 0) atomicAdd(&live_chains, 1);
         a = Ch::A_START_TRANSITION;

@@ -143,6 +143,9 @@ typedef struct fitoct_result {
   int64_t total_leapfrogs;  /* out: sum of n_leapfrog__ over every transition of every chain */
   double kernel_ms;         /* out: device time of the sampler kernel (HIP events) */
   double wall_ms;           /* out: host wall time of the call */
+  int64_t two_ended_transitions; /* out (ABI 6): transitions whose trajectory grew both ends at
+                               once (tiles of one chain; chains alone in a migrating launch's
+                               tail); the draws do not depend on it */
 } fitoct_result;
 
 /* Static description of a planned run. */

@@ -30,7 +30,7 @@ def _run(prob, cfg, migrate):
             os.environ["FITOCT_NO_MIGRATE"] = old
 
 
-@pytest.mark.parametrize("family,N", [("horseshoe", 512), ("normal", 2048)])
+@pytest.mark.parametrize("family,N", [("horseshoe", 512), ("normal", 2048), ("lasso", 1024)])
 def test_migration_preserves_draws_bitwise(family, N):
     prob = _prob(family, N, 15)
     cfg = SamplerConfig(chains=1024, warmup=100, samples=100, seed=21, max_treedepth=7)
@@ -44,3 +44,50 @@ def test_migration_preserves_draws_bitwise(family, N):
     np.testing.assert_array_equal(a.inv_metric, b.inv_metric)
     np.testing.assert_array_equal(a.last_q, b.last_q)
     assert a.total_leapfrogs == b.total_leapfrogs
+
+
+def _run_env(prob, cfg, **env):
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        for k, v in env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        with Plan(prob, cfg) as pl:
+            pl.run()
+            return pl.info, pl.download()
+    finally:
+        for k, v in old.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("family,N,left", [("horseshoe", 2048, None), ("normal", 512, None),
+                                           ("lasso", 1024, "1024")])
+def test_tail_two_ended_preserves_draws_bitwise(family, N, left):
+    """The launch's tail (nuts_device.hip receive_chain, P.tail_bidi): once at most
+    tail_left chains are unfinished (default: one per tile; 1024 = from the first finished
+    chain), a chain alone in its migrating tile recruits two idle receivers of the tile as
+    producers and grows both trajectory ends at once, booking the leaves itself.  Draws,
+    step sizes, metrics, last positions and leapfrog counts equal those of the same launch
+    without it (FITOCT_NO_TAIL_BIDI=1) and without migration at all, and the run reports
+    two-ended transitions."""
+    prob = _prob(family, N, 15)
+    cfg = SamplerConfig(chains=1024, warmup=100, samples=100, seed=23, max_treedepth=8)
+    info, a = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI=None, FITOCT_TAIL_LEFT=left,
+                       FITOCT_NO_MIGRATE=None)
+    _, b = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI="1", FITOCT_TAIL_LEFT=None,
+                    FITOCT_NO_MIGRATE=None)
+    _, c = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI=None, FITOCT_TAIL_LEFT=None,
+                    FITOCT_NO_MIGRATE="1")
+    assert info["chains_per_tile"] == 4 and info["sampler"] == 3
+    assert a.two_ended_transitions > 0, "no tail transition was two-ended"
+    assert b.two_ended_transitions == 0 and c.two_ended_transitions == 0
+    for x in (b, c):
+        np.testing.assert_array_equal(a.draws, x.draws)
+        np.testing.assert_array_equal(a.stepsize, x.stepsize)
+        np.testing.assert_array_equal(a.inv_metric, x.inv_metric)
+        np.testing.assert_array_equal(a.last_q, x.last_q)
+        assert a.total_leapfrogs == x.total_leapfrogs

@@ -56,7 +56,7 @@ def _record(fam):
             return f.read()
     hipcc = B._hipcc()
     out = os.path.join("/tmp", f"fitoct_resources_{fam}_{os.getpid()}.o")
-    cmd = [hipcc, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", f"-DFITOCT_FAMILY={fam}",
+    cmd = [hipcc, *B._KERNEL, f"-DFITOCT_FAMILY={fam}",
            f"-I{B.INCLUDE}", f"-I{B.CSRC}", "--cuda-device-only", "-c", src, "-o", out,
            "-Rpass-analysis=kernel-resource-usage"]
     r = subprocess.run(cmd, capture_output=True, text=True)
