@@ -33,11 +33,7 @@ CLANGXX = "/opt/rocm/lib/llvm/bin/clang++"
 VARIANT = os.environ.get("FITOCT_VARIANT", "")
 ARCH = os.environ.get("FITOCT_ARCH", "gfx950")
 
-# -ffp-contract=on: a * b + c is fused where the source writes it as one expression, never
-# across statements.  HIP's default (fast) let the backend fuse differently in two
-# instantiations of the same sweep (the migrating and the plain kernel at 4 bins per lane,
-# round 5), which broke the bitwise equality of their draws (tests/test_gpu_migration.py).
-_KERNEL = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=on"]
+_KERNEL = [f"--offload-arch={ARCH}", "-O3", "-std=c++17"]
 SOURCES = [
     # (object name, source, compiler, flags).  The sampler source is compiled once
     # per prior family (the family is a template parameter of the kernels).

@@ -182,6 +182,9 @@ constexpr int BD_ENDED = 1 << 20;
 #ifndef FITOCT_BIDI_IDLE_SLEEP
 #define FITOCT_BIDI_IDLE_SLEEP 1
 #endif
+#ifndef FITOCT_SWEEP_FAST_CONTRACT
+#define FITOCT_SWEEP_FAST_CONTRACT 0
+#endif
 #ifndef FITOCT_BIDI_LOOK
 #define FITOCT_BIDI_LOOK 3   // a producer runs at most this many doublings past the booked one
 #endif
@@ -447,6 +450,20 @@ __device__ __forceinline__ void normal_pair(RngKey k, uint32_t c0, uint32_t c1, 
   n1 = rad * sn;
 }
 
+// The sweep's arithmetic is contracted only where the source writes a * b + c as one
+// expression (or calls fma): HIP's default, fast contraction across statements, let the
+// backend fuse the same sweep differently in two kernel instantiations (the migrating and
+// the plain sampler at 4 bins per lane, round 5), which broke the bitwise equality of
+// their draws.  1 + a P(t) is written as an FMA (measured: hand-fusing the four per-bin sums
+// as well costs config 5 7 %, scripts/gpu_r5_variants.sh); config 5 runs 1.7 % below the
+// fast contraction, config 3 0.5 % (profiles/r05_ab_contract.txt).
+// (FITOCT_SWEEP_FAST_CONTRACT: the old contraction, for A/B only)
+#if FITOCT_SWEEP_FAST_CONTRACT
+#pragma clang fp contract(fast)
+#else
+#pragma clang fp contract(on)
+#endif
+
 // ---------------------------------------------------------------------------
 // per-bin arithmetic (the likelihood sweep)
 // ---------------------------------------------------------------------------
@@ -575,9 +592,8 @@ __device__ __forceinline__ R bin_tail(R iL, R cx, R yi, R isu, R th1, R th2, A (
   return w * iL;                                                 // dlp/ddL / (th2 th3) * sigma^2
 }
 template <class R, class A, int NA, bool LAT = false>
-__device__ __forceinline__ R bin_core(R dL, R cx, R yi, R isu, R th1, R th2, R th3, A (&acc)[NA],
-                                      R& umin) {
-  const R u = R(1) + dL;
+__device__ __forceinline__ R bin_core(R u, R cx, R yi, R isu, R th1, R th2, R th3, A (&acc)[NA],
+                                      R& umin) {   // u = 1 + dL
   umin = fmin(umin, u);
   const R L = th3 * u;                                           // decay length theta3*(1+dL)
   const R iL = rcp_<R>(L);
@@ -604,7 +620,7 @@ __device__ __forceinline__ void bin_poly(R cx, R y, R isu, R t, R av, R th1, R t
   R P = cf[NNP - 1];
 #pragma unroll
   for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
-  const R h = bin_core<R, A, 4 + NNP>(av * P, cx, y, isu, th1, th2, th3, acc, umin);
+  const R h = bin_core<R, A, 4 + NNP>(fma(av, P, R(1)), cx, y, isu, th1, th2, th3, acc, umin);
   R p = h * av;
   acc[4] += (A)p;
 #pragma unroll
@@ -627,7 +643,7 @@ __device__ __forceinline__ R bin_poly_fwd(R cx, R y, R isu, R t, R av, R th1, R 
 #pragma unroll
     for (int k = NNP - 2; k >= 0; --k) P = fma(P, t, cf[k]);
   }
-  return bin_core<R, A, 4 + NNP, LAT>(av * P, cx, y, isu, th1, th2, th3, acc, umin) * av;
+  return bin_core<R, A, 4 + NNP, LAT>(fma(av, P, R(1)), cx, y, isu, th1, th2, th3, acc, umin) * av;
 }
 
 // Two bins of bin_poly_fwd sharing one reciprocal: 1/L0 = L1 / (L0 L1), 1/L1 = L0 / (L0 L1)
@@ -691,7 +707,7 @@ __device__ __forceinline__ void bin_rows(R cx, R y, R isu, const R (&Brow)[NNP],
   R dL = R(0);
 #pragma unroll
   for (int k = 0; k < NNP; ++k) dL = fma(Brow[k], yg[k], dL);
-  const R h = bin_core<R, A, 4 + NNP>(dL, cx, y, isu, th1, th2, th3, acc, umin);
+  const R h = bin_core<R, A, 4 + NNP>(R(1) + dL, cx, y, isu, th1, th2, th3, acc, umin);
 #pragma unroll
   for (int k = 0; k < NNP; ++k) acc[4 + k] = fma((A)Brow[k], (A)h, acc[4 + k]);
 }
@@ -971,6 +987,9 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
     if (!(lane & 1) && idx >= 0) part[(c * NGW + wave) * NSLOT + idx] = r;
   }
 }
+
+// (end of the sweep's arithmetic: the sampler's code below keeps HIP's default contraction)
+#pragma clang fp contract(fast)
 
 // ---------------------------------------------------------------------------
 // the chain (one wave; lane = parameter)

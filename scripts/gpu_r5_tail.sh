@@ -8,7 +8,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/r5tail
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_gpu_migration.py tests/test_gpu_spec.py tests/test_gpu_smoke.py \
+  tests/test_gpu_migration.py tests/test_gpu_spec.py tests/test_gpu_smoke.py tests/test_gpu_logp.py \
   > $OUT/pytest.log 2>&1
 rc=$?
 tail -30 $OUT/pytest.log
@@ -22,6 +22,17 @@ run() {   # label, env...
 for r in 1 2; do
   run "tail-on" FITOCT_X=0
   run "tail-off" FITOCT_NO_TAIL_BIDI=1
+  run "tail-on-sweepfast" FITOCT_LIB_PATH=$PWD/ablib/lib_sweepfast.so
 done
-run "tail-left-512" FITOCT_TAIL_LEFT=512
-run "tail-left-128" FITOCT_TAIL_LEFT=128
+run5() {   # label, config, env...
+  local l=$1; local c=$2; shift; shift
+  env "$@" timeout -k 10 200 python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu \
+    2>>$OUT/ab_stderr.log > $OUT/ab.json || exit 1
+  python3 -c "import json;d=json.load(open('$OUT/ab.json'));print('$l config $c', d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])" | tee -a $OUT/ab.txt
+}
+for r in 1 2; do
+  for c in 2 5; do
+    run5 "sweep-on" $c FITOCT_X=0
+    run5 "sweep-fast" $c FITOCT_LIB_PATH=$PWD/ablib/lib_sweepfast.so
+  done
+done

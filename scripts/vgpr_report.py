@@ -9,8 +9,7 @@ import sys
 
 fam = sys.argv[1] if len(sys.argv) > 1 else "2"
 flt = sys.argv[2] if len(sys.argv) > 2 else "nuts_kernel"
-r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on",
-                    f"-DFITOCT_FAMILY={fam}",
+r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-DFITOCT_FAMILY={fam}",
                     "-Iinclude", "-Ifitoct_amd/csrc", "--cuda-device-only", "-c",
                     os.environ.get("SRC", "fitoct_amd/csrc/nuts_device.hip"), "-o", "/tmp/vgpr_report.o",
                     "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("FITOCT_HIPFLAGS", "").split(),
