@@ -182,6 +182,12 @@ constexpr int BD_ENDED = 1 << 20;
 #ifndef FITOCT_BIDI_IDLE_SLEEP
 #define FITOCT_BIDI_IDLE_SLEEP 1
 #endif
+#ifndef FITOCT_MIG_FV3
+#define FITOCT_MIG_FV3 0   // fexp's three-VGPR FMAs in the migrating samplers too (A/B)
+#endif
+#ifndef FITOCT_MIG_KREG
+#define FITOCT_MIG_KREG 0  // migrating samplers keep the speculated leaf in registers (A/B)
+#endif
 #ifndef FITOCT_SWEEP_FAST_CONTRACT
 #define FITOCT_SWEEP_FAST_CONTRACT 0
 #endif
@@ -1024,7 +1030,7 @@ struct Chain {
   // fexp's Horner steps as three-VGPR FMAs (fma_v) in the non-migrating samplers: bitwise
   // the same, configs 2 / 5 +2 / +0.6 %.  The migrating samplers then spill a VGPR (the
   // headline horseshoe one loses 2.2 %, profiles/r03_ab_fmav.txt): they keep the compiler's form
-  static constexpr bool FV3 = !MIG;
+  static constexpr bool FV3 = !MIG || FITOCT_MIG_FV3;
   double krow[KROW ? NNP : 1];
   const AS_LDS double* bv;
   int lane, slot, lc, gid, nct;
@@ -1041,7 +1047,7 @@ struct Chain {
   // V_CA (there is no helper wave, so the next prior part is written only after the
   // bookkeeping), the end-updated p in V_CUR_G (where spec_weight reads it anyway).  No
   // LDS is added: the tile's LDS carve decides how many chains fit (G = 4 at depth 12).
-  static constexpr bool KLDS = MIG;
+  static constexpr bool KLDS = MIG && !FITOCT_MIG_KREG;
   V k_q, k_pe, k_g;
   // (its lp / sum r^2 stay in Sp->cur_lp / cur_s2 until the bookkeeping)
   int k_dirn, k_dn, k_jn;
@@ -2894,7 +2900,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     }
     if (kProfile && wave == 0 && lane == 0 && P.stamps != nullptr) {
       AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)blockIdx.x * NSTAMP;
-      occ_t[occ_k] += (long long)__builtin_amdgcn_s_memrealtime() - occ_last;
+      // (the interval after the last entry: the tile's live count now, normally 0 -- a
+      // tile whose chains have finished waits for migrants, or the launch's end)
+      occ_t[min(max(lds_load(&live_chains), 0), GMAX)] +=
+          (long long)__builtin_amdgcn_s_memrealtime() - occ_last;
       for (int k = 0; k <= GMAX; ++k) {
         o[72 + k] = occ_t[k];
         o[77 + k] = occ_n[k];
