@@ -191,6 +191,14 @@ constexpr int BD_ENDED = 1 << 20;
 #ifndef FITOCT_SWEEP_FAST_CONTRACT
 #define FITOCT_SWEEP_FAST_CONTRACT 0
 #endif
+// poll intervals (s_sleep units of ~64 clocks): an idle gradient wave's ring poll and a
+// two-ended producer's wait for its sweep (A/B knobs)
+#ifndef FITOCT_GRAD_SLEEP
+#define FITOCT_GRAD_SLEEP 1
+#endif
+#ifndef FITOCT_PROD_SLEEP
+#define FITOCT_PROD_SLEEP 1
+#endif
 #ifndef FITOCT_BIDI_LOOK
 #define FITOCT_BIDI_LOOK 3   // a producer runs at most this many doublings past the booked one
 #endif
@@ -2865,7 +2873,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           stop = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(FITOCT_GRAD_SLEEP);
       }
       if (stop) break;
       const int c = (int)(e & 0xFF);
@@ -2978,33 +2986,36 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         wave_fence();
         if (lds_load(&bd[BD_GEN]) != g) continue;   // the start was rewritten while read
         const double e = s ? eps : -eps;
-        int n = 0;
-        for (;;) {
-          bool go = false;
+        // may leaf n of this end grow now: within FITOCT_BIDI_LOOK doublings of the booked one,
+        // and the ring.  Once true it stays true for the transition (the booked depth and the
+        // helper's count only grow), so a check made while a sweep runs holds after it
+        auto may = [&](const int n) -> bool {
+          const int dl = min(pr.uni(*(volatile const AS_LDS int*)&S0.depth) + FITOCT_BIDI_LOOK,
+                             P.max_depth - 1);
+          const int lim = pr.uni(__shfl(cum, dl));
+          const int cons = lds_load(&bd[BD_CONS + s]);
+          return n < lim && n - cons < P.bidi_rb;
+        };
+        auto wait_may = [&](const int n) -> bool {   // false: the tree ended
           Patience w;
-          for (;;) {   // within FITOCT_BIDI_LOOK doublings of the booked one, and the ring
-            if (lds_load(&bd[BD_GEN]) != g) break;
-            const int dl = min(pr.uni(*(volatile const AS_LDS int*)&S0.depth) + FITOCT_BIDI_LOOK,
-                               P.max_depth - 1);
-            const int lim = pr.uni(__shfl(cum, dl));
-            const int cons = lds_load(&bd[BD_CONS + s]);
-            if (n < lim && n - cons < P.bidi_rb) {
-              go = true;
-              break;
-            }
+          for (;;) {
+            if (lds_load(&bd[BD_GEN]) != g) return false;
+            if (may(n)) return true;
             // the other end may grow for long (deep trees, large N).  In effect this wait
             // ends with BD_GEN: its bound outlasts the bound on the whole tree (MIG_WAIT_TICKS
             // from the tree's start), after which BD_GEN changes
-            if (w.expired(2 * MIG_WAIT_TICKS)) break;
+            if (w.expired(2 * MIG_WAIT_TICKS)) return false;
             __builtin_amdgcn_s_sleep(1);
           }
-          if (!go) break;   // the tree ended (next transition or the end)
-          // expl_leapfrog from the last leaf of this end: begin_update_p, update_q
-          Vd<PPL> p1, q1;
+        };
+        // expl_leapfrog from the last leaf of this end (begin_update_p, update_q), staged for
+        // the gradient waves and enqueued; the position-only prior terms overlap the sweep
+        Vd<PPL> p1, q1;
+        auto stage = [&](const Vd<PPL>& qa, const Vd<PPL>& pa, const Vd<PPL>& ga) {
 #pragma unroll
           for (int k = 0; k < PPL; ++k) {
-            p1.a[k] = fma(0.5 * e, gr.a[k], p.a[k]);
-            q1.a[k] = fma(e, minv.a[k] * p1.a[k], q.a[k]);
+            p1.a[k] = fma(0.5 * e, ga.a[k], pa.a[k]);
+            q1.a[k] = fma(e, minv.a[k] * p1.a[k], qa.a[k]);
           }
           pr.write_mp(q1);
           if (lane == 0) {
@@ -3013,7 +3024,17 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
                              __ATOMIC_RELAXED);
           }
           ++epoch;
-          pr.prior_part();   // overlaps the sweep
+        };
+        if (!wait_may(0)) continue;
+        stage(q, p, gr);
+        pr.prior_part();
+        // leaf n is in its sweep here.  Its successor is staged before leaf n's record is
+        // written whenever the successor may grow already (checked while the sweep runs):
+        // the record write and the checks leave the end's critical path
+        for (int n = 0;; ++n) {
+          // (a migrating launch's tail keeps the record-first order: config 3 measured -1.3 %
+          // with the successor staged first, config 2 +13.7 %; profiles/r05_ab_stage.txt)
+          const bool pre = !MIG && may(n + 1);
           bool late = false;
           Patience ws;
           while (lds_load(&grad_cnt[slot]) < (int)(NGW * epoch)) {
@@ -3021,26 +3042,32 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
               late = true;
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(FITOCT_PROD_SLEEP);
           }
           if (late) {
             quit = true;
             break;
           }
           wave_fence();
+          // read with the partial sums (its latency hides in finish_grad's): a leaf the tree
+          // no longer needs is dropped; one published just after the tree ends is ignored
+          // (the count carries its transition)
+          const int gen_now = lds_load(&bd[BD_GEN]);
           Vd<PPL> gn;
           double s2;
           const double lp = pr.finish_grad(gn, s2);
           Vd<PPL> pe;
 #pragma unroll
           for (int k = 0; k < PPL; ++k) pe.a[k] = fma(0.5 * e, gn.a[k], p1.a[k]);   // end_update_p
-          if (lds_load(&bd[BD_GEN]) != g) break;   // the tree has ended: the leaf is not needed
+          if (gen_now != g) break;   // the tree has ended: the leaf is not needed
+          const Vd<PPL> qn = q1;
+          if (pre) stage(qn, pe, gn);
           AS_LDS double* r = pr.brec(s, n);
           const int D = P.D;
 #pragma unroll
           for (int k = 0; k < PPL; ++k) {
             if (pr.ok(k)) {
-              r[pr.idx(k)] = q1.a[k];
+              r[pr.idx(k)] = qn.a[k];
               r[D + pr.idx(k)] = pe.a[k];
               r[2 * D + pr.idx(k)] = gn.a[k];
             }
@@ -3051,10 +3078,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           }
           wave_fence();   // the record lands before its count
           if (lane == 0) __atomic_store_n(&bd[BD_PROD + s], (g << 16) | (n + 1), __ATOMIC_RELAXED);
-          q = q1;
-          p = pe;
-          gr = gn;
-          ++n;
+          if (!pre) {
+            if (!wait_may(n + 1)) break;
+            stage(qn, pe, gn);
+          }
+          pr.prior_part();
         }
       }
     };
