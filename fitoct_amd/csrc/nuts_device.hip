@@ -230,6 +230,19 @@ __device__ __forceinline__ void wave_fence() {
   // compiler may not move memory accesses across this point.
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
+// A wave reading back what its own lanes just stored to LDS: the DS operations of one
+// wave are performed in issue order (the AMDGPU memory model), so only the compiler must
+// keep the order -- no wait for the stores to complete (FITOCT_LOCAL_FENCE=0: the full wait)
+#ifndef FITOCT_LOCAL_FENCE
+#define FITOCT_LOCAL_FENCE 1
+#endif
+__device__ __forceinline__ void wave_order() {
+#if FITOCT_LOCAL_FENCE
+  asm volatile("" ::: "memory");
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+}
 
 // ---------------------------------------------------------------------------
 // chain migration between tiles: agent-scope atomics on global memory (the
@@ -1211,7 +1224,7 @@ struct Chain {
     AS_LDS double* qe = vec(V_QE);
 #pragma unroll
     for (int s = 0; s < PPL; ++s) qs[idx(s)] = q.a[s];
-    wave_fence();   // q of every lane visible: the yGP lanes start at once, in parallel with
+    wave_order();   // q of every lane visible: the yGP lanes start at once, in parallel with
                     // the constrained values below
     double yv = 0.0, hl = 0.0, u = 0.0;
     const int jl = lane < Nn ? lane : 0;
@@ -1241,7 +1254,7 @@ struct Chain {
     }
     sub(5, ts);
     if (poly) {  // c_l = b_l (K^-1 yGP)_l ; K^-1 padded to NNP x NNP
-      wave_fence();
+      wave_order();
       if (lane < NNP) {
         double c0 = 0.0, c1 = 0.0;   // two chains of FMAs: half the dependent latency
 #pragma unroll
@@ -1390,7 +1403,7 @@ struct Chain {
         SUMS[lane] = sl;
       }
       S0 = rl(sl, 0);
-      wave_fence();
+      wave_order();
       double v = 0.0;
       if (lane < NNP) {
         if (poly) {
@@ -1408,7 +1421,7 @@ struct Chain {
         }
       }
       if (FAM == FAM_HORSESHOE) famsum = wave_sum(lane < Nn ? fw * v : 0.0);
-      wave_fence();
+      wave_order();
     }
 #pragma unroll
     for (int s = 0; s < PPL; ++s) {
