@@ -823,7 +823,8 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   // Two-ended trajectories in the tail of a migrating launch (nuts_device.hip receive_chain):
   // the rings live in the producers' own tree-level areas (no LDS added).  Same draws bit
   // for bit.  FITOCT_NO_TAIL_BIDI=1: off; FITOCT_TAIL_LEFT=n: start at n unfinished chains
-  // (default: one per tile).
+  // (default: every chain of the launch -- a chain alone in its tile goes two-ended whenever two
+  // receivers are idle; one per tile measured 1 % slower on config 3).
   k.tail_bidi = 0;
   if (pl->mig_bytes > 0 && k.spec && getenv("FITOCT_NO_TAIL_BIDI") == nullptr) {
     const int rec = (3 * D + 2 + 1) / 2 * 2;
@@ -832,7 +833,7 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
       k.tail_bidi = 1;
       k.bidi_rb = k.bidi_rba = ra;
       k.bidi_rec = rec;
-      k.tail_left = pl->tiles;
+      k.tail_left = k.chains;   // from the start (config 3: +1.0 % over one per tile, profiles/r05_ab_tail_left.txt)
       if (const char* e = getenv("FITOCT_TAIL_LEFT")) k.tail_left = std::max(0, atoi(e));
     }
   }
