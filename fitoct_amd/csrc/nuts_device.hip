@@ -199,6 +199,10 @@ constexpr int BD_ENDED = 1 << 20;
 #ifndef FITOCT_PROD_SLEEP
 #define FITOCT_PROD_SLEEP 1
 #endif
+// the migrating tail's producers: the next leaf staged before the last one's record (A/B knob)
+#ifndef FITOCT_MIG_STAGE_FIRST
+#define FITOCT_MIG_STAGE_FIRST 0
+#endif
 #ifndef FITOCT_BIDI_LOOK
 #define FITOCT_BIDI_LOOK 3   // a producer runs at most this many doublings past the booked one
 #endif
@@ -3047,7 +3051,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         for (int n = 0;; ++n) {
           // (a migrating launch's tail keeps the record-first order: config 3 measured -1.3 %
           // with the successor staged first, config 2 +13.7 %; profiles/r05_ab_stage.txt)
-          const bool pre = !MIG && may(n + 1);
+          const bool pre = (!MIG || FITOCT_MIG_STAGE_FIRST) && may(n + 1);
           bool late = false;
           Patience ws;
           while (lds_load(&grad_cnt[slot]) < (int)(NGW * epoch)) {
