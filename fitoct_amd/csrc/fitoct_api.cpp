@@ -835,6 +835,9 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
       k.bidi_rec = rec;
       k.tail_left = k.chains;   // from the start (config 3: +1.0 % over one per tile, profiles/r05_ab_tail_left.txt)
       if (const char* e = getenv("FITOCT_TAIL_LEFT")) k.tail_left = std::max(0, atoi(e));
+      // FITOCT_TAIL_LIVE=2: also in a tile of two chains (one of them two-ended at a time)
+      k.tail_live = 1;
+      if (const char* e = getenv("FITOCT_TAIL_LIVE")) k.tail_live = std::min(2, std::max(1, atoi(e)));
     }
   }
   *out = guard.release();

@@ -127,6 +127,7 @@ struct KParams {
   // rings of bidi_rb = bidi_rba records in the producers' tree-level areas
   int tail_bidi;
   int tail_left;
+  int tail_live;            // ... in a tile hosting at most this many live chains (1 or 2)
   unsigned long long* bidi_count;   // two-ended transitions of the launch (fitoct_result)
 };
 

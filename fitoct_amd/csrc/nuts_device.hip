@@ -168,7 +168,7 @@ static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
 // producers in place; see receive_chain)
 enum BdWord : int {
   BD_GEN = 0, BD_PROD = 1, BD_CONS = 3, BD_END = 5, BD_EXIT = 6,
-  TW_CLAIM = 7, TW_JOIN = 8, TW_SLOT = 9, TW_CHAIN = 11, TW_LC = 12, BD_N = 16
+  TW_CLAIM = 7, TW_JOIN = 8, TW_SLOT = 9, TW_CHAIN = 11, TW_LC = 12, TW_BUSY = 13, BD_N = 16
 };
 constexpr int BD_GEN_MASK = (1 << 15) - 1;
 // BD_GEN | BD_ENDED: a migrating tile's chain has booked transition BD_GEN's tree to its end
@@ -1795,7 +1795,7 @@ struct Chain {
     FITOCT_MARK(act_begin_subtree);
     if constexpr (kTwoEnded) {
       if (bidi) return bidi_begin();   // reached at depth 0 only: the helper books from there on
-      if (MIG && tail_ready()) return bidi_begin();   // (the chain's own wave books, kernel)
+      if (MIG && tail_ready() && tail_claim()) return bidi_begin();   // (the chain's own wave books, kernel)
     }
     const int d = uni(Sp->depth);
     const double u = uniform(key, (uint32_t)uni(Sp->t), TAG_DIR, (uint32_t)d, 0u);
@@ -2022,11 +2022,19 @@ struct Chain {
     return m < ra ? plv(s) + m * Pr().bidi_rec
                   : HX + (s * (rb - ra) + (m - ra)) * Pr().bidi_rec;
   }
-  // a migrating tile's chain, at the start of a transition (depth 0): two-ended when it is
-  // the tile's only live chain and two idle receivers of the tile have become producers
+  // a migrating tile's chain, at the start of a transition (depth 0): two-ended when the tile
+  // hosts at most P.tail_live live chains, two idle receivers of the tile have become
+  // producers and no other chain of the tile is growing a tree with them (TW_BUSY, claimed
+  // by tail_claim, released when the tree is booked)
   __device__ __forceinline__ bool tail_ready() const {
-    return Pr().tail_bidi != 0 && uni(Sp->depth) == 0 && uni(bd[TW_JOIN]) >= 2 &&
-           uni(__atomic_load_n(live, __ATOMIC_RELAXED)) == 1;
+    const int lv = uni(__atomic_load_n(live, __ATOMIC_RELAXED));
+    return Pr().tail_bidi != 0 && uni(Sp->depth) == 0 && uni(bd[TW_JOIN]) >= 2 && lv >= 1 &&
+           lv <= Pr().tail_live && uni(bd[TW_BUSY]) == 0;
+  }
+  __device__ __forceinline__ bool tail_claim() const {
+    int ok = 0;
+    if (lane == 0) ok = atomicCAS((int*)&bd[TW_BUSY], 0, 1) == 0;
+    return uni(__shfl(ok, 0)) != 0;
   }
   // Book every leaf of transition g in Stan's tree order from the producers' rings: the
   // helper wave of a tile of one chain, or a migrating tile's chain itself.  LB_END, with
@@ -2725,8 +2733,8 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane, volatil
     if (m != 0) break;
     const int done = __builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_DONE]));
     if (done >= P.chains) return -1;
-    if (P.tail_bidi && P.chains - done <= P.tail_left &&
-        __builtin_amdgcn_readfirstlane(*(volatile const AS_LDS int*)live) == 1 &&
+    const int lv = __builtin_amdgcn_readfirstlane(*(volatile const AS_LDS int*)live);
+    if (P.tail_bidi && P.chains - done <= P.tail_left && lv >= 1 && lv <= P.tail_live &&
         __builtin_amdgcn_readfirstlane(bd[TW_CLAIM]) != 3) {
       int r = -1;
       if (lane == 0) {
@@ -3211,7 +3219,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           }
           if constexpr (MIG) {   // the producers stop growing this tree
             wave_fence();
-            if (lane == 0) __atomic_store_n(&bd[BD_GEN], g | BD_ENDED, __ATOMIC_RELAXED);
+            if (lane == 0) {
+              __atomic_store_n(&bd[BD_GEN], g | BD_ENDED, __ATOMIC_RELAXED);
+              __atomic_store_n(&bd[TW_BUSY], 0, __ATOMIC_RELAXED);   // another chain may claim them
+            }
           }
           wave_fence();   // the helper's bookkeeping is read after the end
           // the helper's booked leaves count toward the step bound like the chain's own
