@@ -838,6 +838,8 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
       // FITOCT_TAIL_LIVE=2: also in a tile of two chains (one of them two-ended at a time)
       k.tail_live = 1;
       if (const char* e = getenv("FITOCT_TAIL_LIVE")) k.tail_live = std::min(2, std::max(1, atoi(e)));
+      // FITOCT_TAIL_PROTECT=1: a tile whose lone chain has its producers takes no migrant
+      k.tail_protect = getenv("FITOCT_TAIL_PROTECT") != nullptr && atoi(getenv("FITOCT_TAIL_PROTECT")) != 0;
     }
   }
   *out = guard.release();

@@ -128,6 +128,7 @@ struct KParams {
   int tail_bidi;
   int tail_left;
   int tail_live;            // ... in a tile hosting at most this many live chains (1 or 2)
+  int tail_protect;         // 1: a lone two-ended chain's tile takes no migrant (receive_chain)
   unsigned long long* bidi_count;   // two-ended transitions of the launch (fitoct_result)
 };
 

@@ -2723,7 +2723,7 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane, volatil
     g_add(&M.hdr[MIG_WAITING], 1);
   }
   AS_GLB int* box = &M.mbox[me * GMAX + c];
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   int m = 0;
   // Poll with relaxed loads and acquire once the mailbox is set: an agent-scope acquire
   // invalidates this XCD's L2, and up to hundreds of receivers wait at the end of a launch
@@ -2754,6 +2754,31 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane, volatil
       }
       r = __builtin_amdgcn_readfirstlane(__shfl(r, 0));
       if (r >= 0) return -2 - r;
+    }
+    // (P.tail_protect) the tile's lone chain has its two producers: a migrant here would end
+    // its two-ended trees, so this receiver withdraws its post while the chain is alone, and
+    // posts again once the chain has finished
+    if (P.tail_protect && P.tail_bidi && lv == 1 &&
+        __builtin_amdgcn_readfirstlane(bd[TW_CLAIM]) == 3) {
+      int still = 0;
+      if (lane == 0) {
+        still = (g_and(&M.fmask[me], ~(1 << c)) >> c) & 1;
+        if (still) g_add(&M.hdr[MIG_WAITING], -1);
+      }
+      if (__builtin_amdgcn_readfirstlane(__shfl(still, 0))) {
+        for (;;) {
+          if (__builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_DONE])) >= P.chains) return -1;
+          if (__builtin_amdgcn_readfirstlane(*(volatile const AS_LDS int*)live) != 1) break;
+          __builtin_amdgcn_s_sleep(64);
+        }
+        if (lane == 0) {
+          g_or(&M.fmask[me], 1 << c);
+          g_add(&M.hdr[MIG_WAITING], 1);
+        }
+        t0 = __builtin_amdgcn_s_memrealtime();
+        continue;
+      }
+      // else a donor claimed the slot first: its chain arrives in the mailbox
     }
     if (__builtin_amdgcn_s_memrealtime() - t0 > MIG_WAIT_TICKS) {
       int still = 0;   // withdraw the post unless a donor already claimed it

@@ -64,12 +64,13 @@ def _run_env(prob, cfg, **env):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("family,N,left,live", [("horseshoe", 2048, None, None),
-                                                ("normal", 512, None, None),
-                                                ("lasso", 1024, "256", None),
-                                                ("horseshoe", 2048, None, "2"),
-                                                ("normal", 512, "512", "2")])
-def test_tail_two_ended_preserves_draws_bitwise(family, N, left, live):
+@pytest.mark.parametrize("family,N,left,live,protect", [("horseshoe", 2048, None, None, None),
+                                                        ("normal", 512, None, None, None),
+                                                        ("lasso", 1024, "256", None, None),
+                                                        ("horseshoe", 2048, None, "2", None),
+                                                        ("normal", 512, "512", "2", None),
+                                                        ("horseshoe", 2048, None, None, "1")])
+def test_tail_two_ended_preserves_draws_bitwise(family, N, left, live, protect):
     """The launch's tail (nuts_device.hip receive_chain, P.tail_bidi): once at most
     tail_left chains are unfinished (default: every chain of the launch; 256: one per
     tile), a chain alone in its migrating tile (FITOCT_TAIL_LIVE=2: or sharing it with one
@@ -77,11 +78,12 @@ def test_tail_two_ended_preserves_draws_bitwise(family, N, left, live):
     producers and grows both trajectory ends at once, booking the leaves itself.  Draws,
     step sizes, metrics, last positions and leapfrog counts equal those of the same launch
     without it (FITOCT_NO_TAIL_BIDI=1) and without migration at all, and the run reports
-    two-ended transitions."""
+    two-ended transitions.  FITOCT_TAIL_PROTECT=1: a tile whose lone chain has its producers
+    takes no migrant (its last receiver withdraws its post until the chain finishes)."""
     prob = _prob(family, N, 15)
     cfg = SamplerConfig(chains=1024, warmup=100, samples=100, seed=23, max_treedepth=8)
     info, a = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI=None, FITOCT_TAIL_LEFT=left,
-                       FITOCT_NO_MIGRATE=None, FITOCT_TAIL_LIVE=live)
+                       FITOCT_NO_MIGRATE=None, FITOCT_TAIL_LIVE=live, FITOCT_TAIL_PROTECT=protect)
     _, b = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI="1", FITOCT_TAIL_LEFT=None,
                     FITOCT_NO_MIGRATE=None, FITOCT_TAIL_LIVE=None)
     _, c = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI=None, FITOCT_TAIL_LEFT=None,
