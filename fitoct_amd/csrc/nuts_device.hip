@@ -247,6 +247,21 @@ __device__ __forceinline__ void wave_order() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
 }
+// A wave publishing LDS data to another wave of the tile by a later LDS store or atomic (a
+// sweep's partial sums before grad_cnt, a position's MP before its ring entry, a leaf record
+// before its count): the LDS performs one wave's DS operations in issue order, so a reader
+// that sees the count and then reads the data sees the data.  FITOCT_LDS_INORDER=0: wait for
+// the data stores to complete first (s_waitcnt lgkmcnt(0)).
+#ifndef FITOCT_LDS_INORDER
+#define FITOCT_LDS_INORDER 1
+#endif
+__device__ __forceinline__ void wave_publish() {
+#if FITOCT_LDS_INORDER
+  asm volatile("" ::: "memory");
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+}
 
 // ---------------------------------------------------------------------------
 // chain migration between tiles: agent-scope atomics on global memory (the
@@ -2657,7 +2672,7 @@ struct Chain {
         Sp->prof[1][ai] += 1;
       }
     }
-    wave_fence();
+    wave_publish();   // (the yielded position's MP before the kernel's ring entry)
     return a;
   }
 };
@@ -2944,7 +2959,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       if (P.prior_PD == 0)
         gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1, tid,
                                          lane, wave);
-      wave_fence();   // this wave's PART writes are complete
+      wave_publish();   // this wave's PART writes before its count
       if (wstamp) t_wbusy += (long long)__builtin_amdgcn_s_memtime() - s0w;
       if (lane == 0) {
         if (kProfile)   // latest finisher's time; LDS ops of a wave complete in order
@@ -3126,7 +3141,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             r[3 * D] = lp;
             r[3 * D + 1] = s2;
           }
-          wave_fence();   // the record lands before its count
+          wave_publish();   // the record lands before its count
           if (lane == 0) __atomic_store_n(&bd[BD_PROD + s], (g << 16) | (n + 1), __ATOMIC_RELAXED);
           if (!pre) {
             if (!wait_may(n + 1)) break;
