@@ -2078,7 +2078,7 @@ struct Chain {
       const int r = bidi_book(s, n);
       if (s) ++cons1;
       else ++cons0;
-      wave_fence();
+      wave_publish();
       if (lane == 0) bd[BD_CONS + s] = n + 1;
       if (r == LB_END) return LB_END;
     }
@@ -2118,7 +2118,7 @@ struct Chain {
       bd[TW_CHAIN] = slot;   // the producers read the booked depth and the key from these
       bd[TW_LC] = lc;
     }
-    wave_fence();   // every store above lands before the transition's number
+    wave_publish();   // every store above lands before the transition's number
     if (lane == 0) {
       bd[BD_GEN] = (bd[BD_GEN] & BD_GEN_MASK) % BD_GEN_MASK + 1;
       atomicAdd(Pr().bidi_count, 1ULL);
@@ -3170,7 +3170,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         seen = g;
         wave_fence();   // the transition's start state is read after its number
         ch.bidi_book_tree(g);
-        wave_fence();   // the booking's LDS writes land before the end is published
+        wave_publish();   // the booking's LDS writes land before the end is published
         if (lane == 0) __atomic_store_n(&bd[BD_END], g, __ATOMIC_RELAXED);
       }
     }
@@ -3202,20 +3202,20 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         wave_fence();   // the request's arguments are read after its number
         if (ch.deep) {   // book the handed-over leaf; publish its outcome, then the number
           const int res = ch.deep_book();
-          wave_fence();
+          wave_publish();
           if (lane == 0) {
             __atomic_store_n(&help_res[hs], res, __ATOMIC_RELAXED);
-            wave_fence();
+            wave_publish();
             __atomic_store_n(&help_done[hs], seen, __ATOMIC_RELAXED);
           }
           continue;
         }
         ch.spec_weight();   // first what the chain's bookkeeping waits for
-        wave_fence();
+        wave_publish();
         if (lane == 0) __atomic_store_n(&help_wdone[hs], seen, __ATOMIC_RELAXED);
         ch.prior_and_uniforms(true, lds_load(&help_arg[hs][0]), lds_load(&help_arg[hs][1]),
                               (uint32_t)lds_load(&help_arg[hs][2]));
-        wave_fence();
+        wave_publish();
         if (lane == 0) __atomic_store_n(&help_done[hs], seen, __ATOMIC_RELAXED);
       }
     }
@@ -3258,7 +3258,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
           }
           if constexpr (MIG) {   // the producers stop growing this tree
-            wave_fence();
+            wave_publish();
             if (lane == 0) {
               __atomic_store_n(&bd[BD_GEN], g | BD_ENDED, __ATOMIC_RELAXED);
               __atomic_store_n(&bd[TW_BUSY], 0, __ATOMIC_RELAXED);   // another chain may claim them
@@ -3286,13 +3286,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
                              __ATOMIC_RELAXED);
             if (ch.deep) {
-              wave_fence();   // the hand-off (HX) lands before the request number
+              wave_publish();   // the hand-off (HX) lands before the request number
               __atomic_store_n(&help_req[c], hreq + 1, __ATOMIC_RELAXED);
             } else if (helped) {
               help_arg[c][0] = ch.k_dn;
               help_arg[c][1] = ch.k_jn;
               help_arg[c][2] = (int)ch.k_t;
-              wave_fence();   // the arguments land before the request number
+              wave_publish();   // the arguments land before the request number
               __atomic_store_n(&help_req[c], hreq + 1, __ATOMIC_RELAXED);
             }
           }
