@@ -64,6 +64,7 @@ class Result(C.Structure):
         ("n_cols", C.c_int32), ("iters_saved", C.c_int32), ("dim", C.c_int32),
         ("migrations", C.c_int32), ("total_leapfrogs", C.c_int64), ("kernel_ms", C.c_double),
         ("wall_ms", C.c_double), ("two_ended_transitions", C.c_int64),
+        ("paired_transitions", C.c_int64),
     ]
 
 
@@ -75,6 +76,7 @@ class PlanInfo(C.Structure):
         ("lds_bytes", C.c_int32), ("n_pad", C.c_int32), ("draws_bytes", C.c_int64),
         ("sampler", C.c_int32), ("n_devices", C.c_int32),
         ("two_ended", C.c_int32), ("ring_records", C.c_int32), ("ring_records_in_levels", C.c_int32),
+        ("paired", C.c_int32), ("workgroups", C.c_int32),
     ]
 
 
@@ -203,7 +205,7 @@ def _single_hip_runtime():
         pass
 
 
-ABI_VERSION = 6   # include/fitoct.h FITOCT_ABI_VERSION
+ABI_VERSION = 7   # include/fitoct.h FITOCT_ABI_VERSION
 
 
 def lib():

@@ -197,6 +197,7 @@ class SampleOutput:
     migrations: int = 0        # chains handed between tiles (work balance)
     cfg: object = None         # the SamplerConfig of the run (Stan-CSV header)
     two_ended_transitions: int = 0   # transitions grown at both ends at once (no effect on draws)
+    paired_transitions: int = 0      # ... whose forward end grew in a partner tile (no effect)
 
 
 class Plan:
@@ -300,7 +301,7 @@ class Plan:
                             self.cfg.warmup if self.cfg.save_warmup else 0, eps, minv, lq,
                             int(r.total_leapfrogs), float(r.kernel_ms), 0.0,
                             self.cfg.chain_offset, int(r.migrations), self.cfg,
-                            int(r.two_ended_transitions))
+                            int(r.two_ended_transitions), int(r.paired_transitions))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -369,7 +370,7 @@ class Batch:
                             self.cfg.chain_offset + problem * C_, 0,
                             dataclasses.replace(self.cfg,
                                                 chain_offset=self.cfg.chain_offset + problem * C_),
-                            int(r.two_ended_transitions))
+                            int(r.two_ended_transitions), int(r.paired_transitions))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -421,12 +421,12 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   // (a batch plans every problem's tiles from the batch's total chain count)
   const int gc = g_chains > 0 ? g_chains : chains;
   int G = std::max(1, std::min(GMAX, (gc + ncu - 1) / ncu));
-  while (G > 1 && lds_bytes(pl->ppl, G, max_depth) > 160 * 1024 - 256) --G;
-  if (lds_bytes(pl->ppl, G, max_depth) > 160 * 1024 - 256)
+  // (the kernel's static LDS comes on top of the carve: STATIC_LDS_RESERVE)
+  while (G > 1 && lds_bytes(pl->ppl, G, max_depth) > 160 * 1024 - STATIC_LDS_RESERVE) --G;
+  if (lds_bytes(pl->ppl, G, max_depth) > 160 * 1024 - STATIC_LDS_RESERVE)
     return fail(FITOCT_E_ARG, "max_treedepth too large for the LDS budget");
   k.G = G;
   k.max_depth = max_depth;
-  k.nuts_prio = getenv("FITOCT_NUTS_PRIO") ? atoi(getenv("FITOCT_NUTS_PRIO")) : 3;
   k.spec = 0;   // set below, once migration is decided
   pl->tiles = (chains + G - 1) / G;
   pl->lds = lds_bytes(pl->ppl, G, max_depth);
@@ -458,6 +458,8 @@ void free_plan(fitoct_plan* pl) {
   (void)hipFree(pl->d_mig);
   (void)hipFree(pl->d_mig_img);
   (void)hipFree(pl->d_stamps);
+  (void)hipFree(pl->d_pair_hdr);
+  (void)hipFree(pl->d_pair_buf);
   if (pl->h_prog) (void)hipHostFree(pl->h_prog);
   if (pl->h_cancel) (void)hipHostFree(pl->h_cancel);
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
@@ -679,6 +681,29 @@ int32_t fitoct_plan_create(const fitoct_problem* prob, const fitoct_config* cfg,
 }  // extern "C"
 
 namespace {
+// Paired tiles (nuts_device.hip "paired tiles"): a launch of one-chain tiles with two-ended
+// trajectories whose 2 x tiles (in whole groups of 8 + 8 blocks) fit on the chip grows each
+// trajectory's forward end in a partner tile with its own gradient waves, instead of sharing
+// the tile's.  Same draws bit for bit: the partner runs the same producer on the same values.
+// A partner that does not get a CU at launch leaves its primary to grow both ends (the pair's
+// hand-shake), so this is safe on a shared GPU too.  FITOCT_NO_PAIR=1: off.
+bool want_pairs(const KParams& k, int tiles, int ncu) {
+  return k.bidi && k.G == 1 && pair_grid(tiles) <= ncu && getenv("FITOCT_NO_PAIR") == nullptr;
+}
+// the pairs' hand-off words and buffers for `tiles` tiles; sets every k.pair_* but the count
+int alloc_pairs(KParams& k, int tiles, int ppl, int** hdr, double** buf) {
+  k.pair = 1;
+  k.pair_tiles = tiles;
+  k.pair_stride = (PAIR_START_DOUBLES + WAVE * ppl * 4 + k.bidi_rb * k.bidi_rec + 15) / 16 * 16;
+  HIP_TRY(hipMalloc(hdr, sizeof(int) * PAIR_HDR_INTS * (size_t)tiles));
+  HIP_TRY(hipMalloc(buf, sizeof(double) * (size_t)k.pair_stride * tiles));
+  k.pair_hdr = *hdr;
+  k.pair_buf = *buf;
+  const char* t = getenv("FITOCT_TEST_PAIR_ABSENT");   // test hook: partners never join
+  k.pair_test_absent = (t && atoi(t) != 0) ? 1 : 0;
+  return FITOCT_OK;
+}
+
 int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chains,
                 int force_bpt, fitoct_plan** out) {
   if (!out) return fail(FITOCT_E_ARG, "out is NULL");
@@ -726,8 +751,8 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
     HIP_TRY(hipMalloc(&pl->d_stack, sizeof(double) * (size_t)C * (cfg->max_treedepth + 1) * POOL_VECS * vlen));
     HIP_TRY(hipMalloc(&pl->d_fin, sizeof(double) * (size_t)C * (1 + 2 * D)));
     HIP_TRY(hipMalloc(&pl->d_status, sizeof(int) * C));
-    // [chains] leapfrogs per chain, then the two-ended transition count of the launch
-    HIP_TRY(hipMalloc(&pl->d_leap, sizeof(long long) * (C + 1)));
+    // [chains] leapfrogs per chain, then the launch's two-ended and paired transition counts
+    HIP_TRY(hipMalloc(&pl->d_leap, sizeof(long long) * (C + 2)));
     HIP_TRY(hipEventCreate(&pl->ev0));
     HIP_TRY(hipEventCreate(&pl->ev1));
     return FITOCT_OK;
@@ -741,6 +766,7 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   k.chain_status = pl->d_status;
   k.leapfrogs = pl->d_leap;
   k.bidi_count = (unsigned long long*)(pl->d_leap + C);
+  k.pair_count = (unsigned long long*)(pl->d_leap + C + 1);
   if (g_chains == 0) {   // progress / cancellation (fitoct_plan_poll / _cancel); batch: off
     auto prog_setup = [&]() -> int {
       HIP_TRY(hipHostMalloc((void**)&pl->h_prog, sizeof(int) * C,
@@ -805,7 +831,7 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   if (k.spec && k.G == 1 && pl->mig_bytes == 0 && getenv("FITOCT_NO_BIDI") == nullptr) {
     const int rec = (3 * D + 2 + 1) / 2 * 2;   // doubles, 16-byte records
     const int base = lds_bytes(pl->ppl, 3, k.max_depth);
-    const int avail = 160 * 1024 - 256 - 1024 - base;   // 1 KB for the kernel's static LDS
+    const int avail = 160 * 1024 - 256 - STATIC_LDS_RESERVE - base;
     const int ra = lvl_doubles(pl->ppl, k.max_depth) / rec;
     int rb = std::min(256, ra + (avail > 0 ? avail / (2 * rec * 8) : 0));
     if (const char* e = getenv("FITOCT_BIDI_RB")) rb = std::min(rb, std::max(1, atoi(e)));
@@ -835,12 +861,12 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
       k.bidi_rec = rec;
       k.tail_left = k.chains;   // from the start (config 3: +1.0 % over one per tile, profiles/r05_ab_tail_left.txt)
       if (const char* e = getenv("FITOCT_TAIL_LEFT")) k.tail_left = std::max(0, atoi(e));
-      // FITOCT_TAIL_LIVE=2: also in a tile of two chains (one of them two-ended at a time)
-      k.tail_live = 1;
-      if (const char* e = getenv("FITOCT_TAIL_LIVE")) k.tail_live = std::min(2, std::max(1, atoi(e)));
-      // FITOCT_TAIL_PROTECT=1: a tile whose lone chain has its producers takes no migrant
-      k.tail_protect = getenv("FITOCT_TAIL_PROTECT") != nullptr && atoi(getenv("FITOCT_TAIL_PROTECT")) != 0;
     }
+  }
+  // (a batch pairs its tiles itself: fitoct_batch_create)
+  if (g_chains == 0 && want_pairs(k, pl->tiles, pl->ncu)) {
+    rc = alloc_pairs(k, pl->tiles, pl->ppl, &pl->d_pair_hdr, &pl->d_pair_buf);
+    if (rc) return rc;
   }
   *out = guard.release();
   return FITOCT_OK;
@@ -868,9 +894,12 @@ int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
     info->lds_bytes = pl->lds;
     info->n_pad = pl->kp.n_pad;
     info->draws_bytes = (int64_t)pl->draws_bytes;
-    info->two_ended = pl->kp.bidi;
-    info->ring_records = pl->kp.bidi ? pl->kp.bidi_rb : 0;
-    info->ring_records_in_levels = pl->kp.bidi ? pl->kp.bidi_rba : 0;
+    const bool te = pl->kp.bidi || pl->kp.tail_bidi;
+    info->two_ended = pl->kp.bidi ? 1 : pl->kp.tail_bidi ? 2 : 0;
+    info->ring_records = te ? pl->kp.bidi_rb : 0;
+    info->ring_records_in_levels = te ? pl->kp.bidi_rba : 0;
+    info->paired = pl->kp.pair;
+    info->workgroups = pl->grid();
     return FITOCT_OK;
   });
 }
@@ -921,8 +950,10 @@ int32_t fitoct_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
     KParams k = pl->kp;
     k.draws = dst;
     HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * k.chains, st));
-    HIP_TRY(hipMemsetAsync(k.bidi_count, 0, sizeof(long long), st));
+    HIP_TRY(hipMemsetAsync(k.bidi_count, 0, 2 * sizeof(long long), st));   // + pair_count
     if (pl->d_mig) HIP_TRY(hipMemsetAsync(pl->d_mig, 0, pl->mig_bytes, st));
+    if (k.pair)   // every word the pairs poll: zero before every launch
+      HIP_TRY(hipMemsetAsync(k.pair_hdr, 0, sizeof(int) * PAIR_HDR_INTS * (size_t)k.pair_tiles, st));
     const bool want_stamps = getenv("FITOCT_STAMPS") != nullptr;   // diagnostic only
     if (want_stamps) {
       if (!pl->d_stamps) HIP_TRY(hipMalloc(&pl->d_stamps, sizeof(long long) * NSTAMP * pl->tiles));
@@ -933,7 +964,7 @@ int32_t fitoct_plan_launch(fitoct_plan* pl, void* d_draws, void* stream) {
     HIP_TRY(hipEventRecord(pl->ev0, st));
     if (!pl->d_kp) HIP_TRY(hipMalloc(&pl->d_kp, sizeof(KParams)));
     HIP_TRY(hipMemcpyAsync(pl->d_kp, &k, sizeof(KParams), hipMemcpyHostToDevice, st));
-    HIP_TRY(launch(false, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->tiles, st));
+    HIP_TRY(launch(false, pl->mixed, pl->bpt, pl->nnp, k, pl->d_kp, pl->grid(), st));
     HIP_TRY(hipEventRecord(pl->ev1, st));
     pl->last_draws = dst;
     pl->launched = true;
@@ -1090,6 +1121,29 @@ int32_t fitoct_plan_wait(fitoct_plan* pl) {
           fprintf(stderr, " k=%d %.4f/%.4f", k, ot[k] / std::max(st, 1.0), on[k] / std::max(sn, 1.0));
         fprintf(stderr, "\n");
       }
+      if (pl->kp.bidi) {   // two-ended roles (tiles of one chain; paired: the forward end's
+                           // producer runs in the partner tile)
+        double hb = 0, hw = 0, hn = 0, hi = 0, pe[2][4] = {{0}};
+        for (int t = 0; t < pl->tiles; ++t) {
+          const long long* o = h.data() + (size_t)NSTAMP * t;
+          hb += o[84];
+          hw += o[85];
+          hn += o[86];
+          hi += o[87];
+          for (int s = 0; s < 2; ++s)
+            for (int k = 0; k < 4; ++k) pe[s][k] += o[88 + 4 * s + k];
+        }
+        fprintf(stderr,
+                "[fitoct stamps] booking wave per booked leaf: busy %.0f, waiting for its record %.0f "
+                "(leaves booked per tile %.0f, idle between trees %.0f per tile)\n",
+                hb / std::max(hn, 1.0), hw / std::max(hn, 1.0), hn / pl->tiles, hi / pl->tiles);
+        for (int s = 0; s < 2; ++s)
+          fprintf(stderr,
+                  "[fitoct stamps] producer of end %d per produced leaf: waiting for its sweep %.0f, "
+                  "for lookahead / ring room %.0f, in trees %.0f (leaves per tile %.0f)\n",
+                  s, pe[s][0] / std::max(pe[s][2], 1.0), pe[s][1] / std::max(pe[s][2], 1.0),
+                  pe[s][3] / std::max(pe[s][2], 1.0), pe[s][2] / pl->tiles);
+      }
     }
     pl->ran = true;
     return FITOCT_OK;
@@ -1140,6 +1194,8 @@ int32_t fitoct_plan_download(fitoct_plan* pl, fitoct_result* res) {
     long long nb = 0;
     HIP_TRY(hipMemcpy(&nb, k.bidi_count, sizeof(long long), hipMemcpyDeviceToHost));
     res->two_ended_transitions = nb;
+    HIP_TRY(hipMemcpy(&nb, k.pair_count, sizeof(long long), hipMemcpyDeviceToHost));
+    res->paired_transitions = nb;
     if (bad >= 0)
       return fail(st[bad], "chain " + std::to_string(k.chain_offset + bad) + " failed with status " +
                                std::to_string(st[bad]));
@@ -1213,6 +1269,8 @@ void free_batch(fitoct_batch* b) {
   for (fitoct_plan* pl : b->plans) free_plan(pl);
   (void)hipFree(b->d_kp);
   (void)hipFree(b->d_map);
+  (void)hipFree(b->d_pair_hdr);
+  (void)hipFree(b->d_pair_buf);
   (void)hipFree(b->d_draws);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
@@ -1300,6 +1358,15 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
       HIP_TRY(hipMalloc(&b->d_map, sizeof(int) * map.size()));
       HIP_TRY(hipMemcpy(b->d_map, map.data(), sizeof(int) * map.size(), hipMemcpyHostToDevice));
       HIP_TRY(hipMalloc(&b->d_kp, sizeof(KParams) * n_problems));
+      // paired tiles over the whole batch (one-chain tiles: config 5's 4- and 8-GPU shares)
+      {
+        KParams kq = b->plans[0]->kp;
+        if (want_pairs(kq, b->tiles, b->plans[0]->ncu)) {
+          const int rc2 = alloc_pairs(kq, b->tiles, b->plans[0]->ppl, &b->d_pair_hdr, &b->d_pair_buf);
+          if (rc2) return rc2;
+          b->pair_stride = kq.pair_stride;
+        }
+      }
       // cancellation flag (set by the multi-device layer when another device fails)
       HIP_TRY(hipHostMalloc((void**)&b->h_cancel, sizeof(int),
                             hipHostMallocMapped | hipHostMallocCoherent));
@@ -1324,6 +1391,8 @@ int32_t fitoct_batch_get_info(const fitoct_batch* b, fitoct_plan_info* info) {
     if (rc) return rc;
     info->chains = b->cfg.chains * (int)b->plans.size();
     info->tiles = b->tiles;
+    info->paired = b->d_pair_hdr ? 1 : 0;
+    info->workgroups = b->d_pair_hdr ? pair_grid(b->tiles) : b->tiles;
     info->draws_bytes = (int64_t)(b->per_bytes * b->plans.size());
     return FITOCT_OK;
   });
@@ -1348,12 +1417,24 @@ int fitoct::batch_run_single(fitoct_batch* b, void* d_draws, void* stream) {
       kp[p].cancel = b->d_cancel;
       pl->last_draws = kp[p].draws;
       HIP_TRY(hipMemsetAsync(pl->d_status, 0, sizeof(int) * pl->kp.chains, st));
-      HIP_TRY(hipMemsetAsync(pl->kp.bidi_count, 0, sizeof(long long), st));
+      HIP_TRY(hipMemsetAsync(pl->kp.bidi_count, 0, 2 * sizeof(long long), st));   // + pair_count
+      if (b->d_pair_hdr) {   // paired tiles: every problem's block names the batch's pairs
+        kp[p].pair = 1;
+        kp[p].pair_tiles = b->tiles;
+        kp[p].pair_stride = b->pair_stride;
+        kp[p].pair_hdr = b->d_pair_hdr;
+        kp[p].pair_buf = b->d_pair_buf;
+        const char* t = getenv("FITOCT_TEST_PAIR_ABSENT");
+        kp[p].pair_test_absent = (t && atoi(t) != 0) ? 1 : 0;
+      }
     }
+    if (b->d_pair_hdr)
+      HIP_TRY(hipMemsetAsync(b->d_pair_hdr, 0, sizeof(int) * PAIR_HDR_INTS * (size_t)b->tiles, st));
     HIP_TRY(hipMemcpyAsync(b->d_kp, kp.data(), sizeof(KParams) * P, hipMemcpyHostToDevice, st));
     const fitoct_plan* p0 = b->plans[0];
     HIP_TRY(hipEventRecord(b->ev0, st));
-    HIP_TRY(launch(false, p0->mixed, p0->bpt, p0->nnp, kp[0], b->d_kp, b->tiles, st, b->d_map));
+    HIP_TRY(launch(false, p0->mixed, p0->bpt, p0->nnp, kp[0], b->d_kp,
+                   b->d_pair_hdr ? pair_grid(b->tiles) : b->tiles, st, b->d_map));
     HIP_TRY(hipEventRecord(b->ev1, st));
     HIP_TRY(hipEventSynchronize(b->ev1));
     float ms = 0.f;

@@ -20,7 +20,15 @@ constexpr int NSLOT = 32;         // reduced sums per chain (4 + NNP <= 32)
 constexpr int MPW = 32;           // model-parameter words per chain (theta[3], pad, yGP[NNP])
 constexpr int POOL_VECS = 2;      // vectors per proposal-pool slot in HBM (q, grad)
 constexpr int KMAX = 24;          // max GP control points (K^-1 tile in LDS)
-constexpr int NSTAMP = 84;        // diagnostic stamps per tile (FITOCT_STAMPS)
+constexpr int NSTAMP = 100;        // diagnostic stamps per tile (FITOCT_STAMPS)
+constexpr int PAIR_HDR_INTS = 64; // paired tiles: hand-off words per pair (nuts_device.hip PairHdr)
+constexpr int PAIR_START_DOUBLES = 8;   // ... and per pair in pair_buf: the start's 4 vectors, then
+                                        // these scalars, then the ring
+// the kernel's static LDS (rings, hand-off words, counters: 352 B measured, the
+// -Rpass-analysis "LDS Size" of every sampler instantiation), reserved in every LDS plan
+constexpr int STATIC_LDS_RESERVE = 1024;
+// paired tiles: blocks launched for `tiles` tiles (groups of 8 primaries + 8 partners)
+inline int pair_grid(int tiles) { return 16 * ((tiles + 7) / 8); }
 
 // how a tile evaluates the GP modulation dL = B yGP and its adjoint B^T h.
 // With BPT > 0 a lane's bins stay in VGPRs for the whole run, with BPT == 0 the
@@ -98,7 +106,6 @@ struct KParams {
   int* mig;                 // MigCtrl header | load | free_mask | mailbox (see MigCtrl)
   double* mig_img;          // [tiles * GMAX][mig_img_words] chain images in flight
   int mig_tiles, mig_img_words;
-  int nuts_prio;            // s_setprio of the NUTS waves (0..3)
   int spec;                 // 1: the speculative-leaf sampler (nuts_device.hip leaf_spec)
   int spec_live;            // ... a chain speculates while its tile hosts <= spec_live live
                             // chains (tiles of one chain: always, with a helper wave)
@@ -127,9 +134,17 @@ struct KParams {
   // rings of bidi_rb = bidi_rba records in the producers' tree-level areas
   int tail_bidi;
   int tail_left;
-  int tail_live;            // ... in a tile hosting at most this many live chains (1 or 2)
-  int tail_protect;         // 1: a lone two-ended chain's tile takes no migrant (receive_chain)
   unsigned long long* bidi_count;   // two-ended transitions of the launch (fitoct_result)
+  // ---- paired tiles (one-chain tiles with two-ended trajectories, 2 x tiles <= CUs; 0: off) ----
+  // the forward end of each tile's trajectories grows in a partner tile with its own gradient
+  // waves (nuts_device.hip "paired tiles"); the grid is 16 * ceil(pair_tiles / 8) blocks
+  int pair;
+  int pair_tiles;           // tiles of the launch (the tile map's entries)
+  int pair_stride;          // doubles per pair in pair_buf: start (4 vectors + 8) | bidi_rb records
+  int pair_test_absent;     // test hook (FITOCT_TEST_PAIR_ABSENT): partners leave at once
+  int* pair_hdr;            // [pair_tiles][PAIR_HDR_INTS] hand-off words, zeroed per launch
+  double* pair_buf;         // [pair_tiles][pair_stride]
+  unsigned long long* pair_count;   // transitions grown by a pair (fitoct_result)
 };
 
 }  // namespace fitoct

@@ -407,10 +407,12 @@ int group_plan_download(fitoct_plan* pl, fitoct_result* res) {
   res->migrations = 0;
   res->total_leapfrogs = 0;
   res->two_ended_transitions = 0;
+  res->paired_transitions = 0;
   for (const fitoct_result& s : sub) {
     res->migrations += s.migrations;
     res->total_leapfrogs += s.total_leapfrogs;
     res->two_ended_transitions += s.two_ended_transitions;
+    res->paired_transitions += s.paired_transitions;
   }
   return rc;
 }

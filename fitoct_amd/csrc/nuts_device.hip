@@ -67,38 +67,12 @@ namespace fitoct {
 using KPc = const AS_CST KParams;
 
 enum { FAM_NORMAL = 0, FAM_LASSO = 1, FAM_HORSESHOE = 2, FAM_MONO = 3 };
-// FITOCT_PAIRED_BINS=0 builds the 8-bins-per-lane sweep with one reciprocal per bin and
-// Taylor-12 exp, as the other widths (A/B of bin_poly_fwd2)
-#ifndef FITOCT_PAIRED_BINS
-#define FITOCT_PAIRED_BINS 1
-#endif
-// Sweeps of at most 2 bins per lane (N <= 512: configs 2 and 5) are latency-bound (two
-// independent bins per lane, then the reduction): the basis polynomial and exp are then
-// evaluated by Estrin's scheme (dependency depth 4-5 instead of 12-14, three more
-// multiplies).  FITOCT_LAT_SWEEP=0 builds the Horner forms there too (A/B).
-#ifndef FITOCT_LAT_SWEEP
-#define FITOCT_LAT_SWEEP 1
-#endif
-// 16 bins per lane (config 4): bins in groups of FITOCT_BPT16_GROUP whose moments are
-// formed per group, and (FITOCT_BPT16_PAIRS) pairs sharing one reciprocal
-#ifndef FITOCT_BPT16_GROUP
-#define FITOCT_BPT16_GROUP 8
-#endif
-#ifndef FITOCT_BPT16_PAIRS
-#define FITOCT_BPT16_PAIRS 0
-#endif
-// deep speculation in tiles of one chain: the helper wave does the whole bookkeeping of leaf
-// k (merge uniforms, weight, U-turn checks, merges, push, top merge) while the chain's wave
-// completes gradient k + 1
-#ifndef FITOCT_DEEP_SPEC
-#define FITOCT_DEEP_SPEC 1
-#endif
-#ifndef FITOCT_NT_DRAWS
-#define FITOCT_NT_DRAWS 1
-#endif
-#ifndef FITOCT_BPT16_OPAQUE
-#define FITOCT_BPT16_OPAQUE 1
-#endif
+// (round 6: the A/B switches measured "off" or "rejected" in DESIGN.md §4 are gone from
+// the kernel; what is left compiles to the measured defaults.  The only remaining build
+// switches are the ordering fallbacks FITOCT_LOCAL_FENCE / FITOCT_LDS_INORDER and the
+// profiling build FITOCT_PROFILE.)
+// 16 bins per lane (config 4): moments are formed per group of 8 bins
+constexpr int BPT16_GROUP = 8;
 
 // Cycle stamps (FITOCT_STAMPS) exist only in a profiling build
 // (FITOCT_PROFILE=1 python -m fitoct_amd.build): the production kernels carry
@@ -174,38 +148,9 @@ constexpr int BD_GEN_MASK = (1 << 15) - 1;
 // BD_GEN | BD_ENDED: a migrating tile's chain has booked transition BD_GEN's tree to its end
 // (its producers stop, and wait for the next transition or the launch's end)
 constexpr int BD_ENDED = 1 << 20;
-// the chain's wave while the producers and the helper grow a tree: its priority (-1: the NUTS
-// priority) and poll interval (A/B knobs)
-#ifndef FITOCT_BIDI_IDLE_PRIO
-#define FITOCT_BIDI_IDLE_PRIO -1
-#endif
-#ifndef FITOCT_BIDI_IDLE_SLEEP
-#define FITOCT_BIDI_IDLE_SLEEP 1
-#endif
-#ifndef FITOCT_MIG_FV3
-#define FITOCT_MIG_FV3 0   // fexp's three-VGPR FMAs in the migrating samplers too (A/B)
-#endif
-#ifndef FITOCT_MIG_KREG
-#define FITOCT_MIG_KREG 0  // migrating samplers keep the speculated leaf in registers (A/B)
-#endif
-#ifndef FITOCT_SWEEP_FAST_CONTRACT
-#define FITOCT_SWEEP_FAST_CONTRACT 0
-#endif
-// poll intervals (s_sleep units of ~64 clocks): an idle gradient wave's ring poll and a
-// two-ended producer's wait for its sweep (A/B knobs)
-#ifndef FITOCT_GRAD_SLEEP
-#define FITOCT_GRAD_SLEEP 1
-#endif
-#ifndef FITOCT_PROD_SLEEP
-#define FITOCT_PROD_SLEEP 1
-#endif
-// the migrating tail's producers: the next leaf staged before the last one's record (A/B knob)
-#ifndef FITOCT_MIG_STAGE_FIRST
-#define FITOCT_MIG_STAGE_FIRST 0
-#endif
-#ifndef FITOCT_BIDI_LOOK
-#define FITOCT_BIDI_LOOK 3   // a producer runs at most this many doublings past the booked one
-#endif
+// a producer runs at most this many doublings past the booked one (lookahead 1 / 2 / 5
+// measured -1.0 / -0.2 / +-0 % on config 2, profiles/r05_ab_stage.txt)
+constexpr int BIDI_LOOK = 3;
 
 constexpr long long SPIN_LIMIT = 1LL << 26;   // polls (~2 s) before a wait reads the clock
 constexpr unsigned long long TICKS_PER_S = 100000000ULL;   // s_memrealtime: 100 MHz
@@ -303,6 +248,48 @@ struct MigView {   // KParams::mig carved per MigCtrl
         mbox(fmask + tiles) {}
 };
 constexpr unsigned long long MIG_WAIT_TICKS = 120ULL * TICKS_PER_S;
+
+// ---------------------------------------------------------------------------
+// paired tiles (KParams::pair): the forward end of a one-chain tile's two-ended trajectories
+// grows in a partner tile, with its own four gradient waves.  Everything crossing between
+// the two workgroups is a write-through (sc1) agent-scope store, drained by the storing wave
+// (s_waitcnt vmcnt(0)) before the one word that publishes it, and read with sc1 loads only
+// (relaxed agent-scope atomics: global_load / global_store ... sc1, no L1 copy on either
+// side), so no L2 write-back or invalidation is needed whichever XCDs the two tiles sit on.
+// Per pair: PAIR_HDR_INTS hand-off words (zeroed before every launch), then in pair_buf
+// the transition's start and a ring of bidi_rb leaf records.
+// ---------------------------------------------------------------------------
+enum PairHdr : int {
+  // primary -> partner: the transition (its start is in pair_buf; -1: the chain finished),
+  // the helper's booked leaves of the forward end and the booked depth, each (gen << 16) | v;
+  // the chain's index and the transition's number t
+  PH_GEN = 0, PH_CONS = 1, PH_DEPTH = 2, PH_LC = 3, PH_T = 4,
+  PH_COUNT = 32,   // partner -> primary: (gen << 16) | forward-end records in the ring
+  PH_STATE = 48    // PairState bits (both, atomics); PAIR_HDR_INTS words per pair (kernel_params.h)
+};
+// The pair's hand-shake: the primary marks START when it begins; the partner joins (START ->
+// START | JOIN) only if the primary has begun, else marks LOCAL and leaves; the primary decides
+// at its chain's first transition (START -> START | LOCAL unless the partner has joined).  So
+// a partner that is not resident (a busy GPU) never holds up its primary, and a primary only
+// ever waits for a partner that is running: the unpaired tile grows both ends itself.
+enum PairState : int { PS_START = 1, PS_JOIN = 2, PS_LOCAL = 4 };
+constexpr unsigned long long PAIR_JOIN_TICKS = 10000;   // 100 us (s_memrealtime: 100 MHz)
+__device__ __forceinline__ void x_st(AS_GLB double* p, double v) {
+  __hip_atomic_store((AS_GLB unsigned long long*)p, __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double x_ld(const AS_GLB double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load((AS_GLB unsigned long long*)p,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void x_sti(AS_GLB int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int x_ldi(AS_GLB int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every sc1 store of this wave has reached memory (before the word that publishes them)
+__device__ __forceinline__ void x_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------------------
 // cross-lane moves of doubles without LDS (DPP row ops, gfx950 permlane swaps)
@@ -503,12 +490,7 @@ __device__ __forceinline__ void normal_pair(RngKey k, uint32_t c0, uint32_t c1, 
 // their draws.  1 + a P(t) is written as an FMA (measured: hand-fusing the four per-bin sums
 // as well costs config 5 7 %, scripts/gpu_r5_variants.sh); config 5 runs 1.7 % below the
 // fast contraction, config 3 0.5 % (profiles/r05_ab_contract.txt).
-// (FITOCT_SWEEP_FAST_CONTRACT: the old contraction, for A/B only)
-#if FITOCT_SWEEP_FAST_CONTRACT
-#pragma clang fp contract(fast)
-#else
 #pragma clang fp contract(on)
-#endif
 
 // ---------------------------------------------------------------------------
 // per-bin arithmetic (the likelihood sweep)
@@ -937,31 +919,20 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
       const double tmax = P.geo_tmax;
       // opaque per sweep: c*x_b and t_b are formed inside the sweep, as the compact layout
       // intends, instead of being hoisted out of the sweep loop (32 more live doubles)
-      if constexpr (FITOCT_BPT16_OPAQUE) asm volatile("" : "+v"(cx0), "+v"(t0));
-      // the lane's bins in groups of NQ (moments per group: NQ weights live at a time)
-      constexpr int NQ = FITOCT_BPT16_GROUP;
+      asm volatile("" : "+v"(cx0), "+v"(t0));
+      // the lane's bins in groups of NQ (moments per group: NQ weights live at a time);
+      // one reciprocal per bin (pairs sharing one measured 3 % slower here)
+      constexpr int NQ = BPT16_GROUP;
 #pragma unroll
       for (int q = 0; q < 16 / NQ; ++q) {
         double w[NQ];
-        if constexpr (FITOCT_BPT16_PAIRS) {
 #pragma unroll
-          for (int b = 0; b < NQ; b += 2) {
-            const int bb = q * NQ + b;
-            bin_poly_fwd2<R, NNP, double>(cx0 + P.geo_dcx[bb], bins.y[bb], bins.isu[bb],
-                                          fmin(t0 * P.geo_R[bb], tmax), bins.row[bb][1],
-                                          cx0 + P.geo_dcx[bb + 1], bins.y[bb + 1], bins.isu[bb + 1],
-                                          fmin(t0 * P.geo_R[bb + 1], tmax), bins.row[bb + 1][1],
-                                          th1, th2, th3, cf, acc, umin, w[b], w[b + 1]);
-          }
-        } else {
-#pragma unroll
-          for (int b = 0; b < NQ; ++b) {
-            const int bb = q * NQ + b;
-            const double cxb = cx0 + P.geo_dcx[bb];
-            const double tb = fmin(t0 * P.geo_R[bb], tmax);
-            w[b] = bin_poly_fwd<R, NNP, double>(cxb, bins.y[bb], bins.isu[bb], tb,
-                                                bins.row[bb][1], th1, th2, th3, cf, acc, umin);
-          }
+        for (int b = 0; b < NQ; ++b) {
+          const int bb = q * NQ + b;
+          const double cxb = cx0 + P.geo_dcx[bb];
+          const double tb = fmin(t0 * P.geo_R[bb], tmax);
+          w[b] = bin_poly_fwd<R, NNP, double>(cxb, bins.y[bb], bins.isu[bb], tb,
+                                              bins.row[bb][1], th1, th2, th3, cf, acc, umin);
         }
         moments_geo_add<NQ, NNP>(P, q ? t0 * P.geo_R[q * NQ] : t0, w, acc);
       }
@@ -971,7 +942,7 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
         // 8 bins per lane (the headline shape, N = 2048): bins in pairs sharing one
         // reciprocal, exp by a degree-11 polynomial (A/B: config 3 +1.7 %, configs 2 / 5
         // within noise; at 16 bins the pairs spill)
-        if constexpr (BPT == 8 && FITOCT_PAIRED_BINS) {
+        if constexpr (BPT == 8) {
 #pragma unroll
           for (int b = 0; b < BPT; b += 2)
             bin_poly_fwd2<R, NNP, double>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b][0],
@@ -979,7 +950,9 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                                           bins.isu[b + 1], bins.row[b + 1][0], bins.row[b + 1][1],
                                           th1, th2, th3, cf, acc, umin, w[b], w[b + 1]);
         } else {
-          constexpr bool LAT = FITOCT_LAT_SWEEP && BPT <= 2;   // latency-bound short sweeps
+          // sweeps of at most 2 bins per lane (N <= 512: configs 2 and 5) are latency-bound:
+          // the basis polynomial and exp by Estrin's scheme (config 5 +1.8 %)
+          constexpr bool LAT = BPT <= 2;
 #pragma unroll
           for (int b = 0; b < BPT; ++b)
             w[b] = bin_poly_fwd<R, NNP, double, LAT>(bins.cx[b], bins.y[b], bins.isu[b],
@@ -1070,7 +1043,7 @@ struct Chain {
   // fexp's Horner steps as three-VGPR FMAs (fma_v) in the non-migrating samplers: bitwise
   // the same, configs 2 / 5 +2 / +0.6 %.  The migrating samplers then spill a VGPR (the
   // headline horseshoe one loses 2.2 %, profiles/r03_ab_fmav.txt): they keep the compiler's form
-  static constexpr bool FV3 = !MIG || FITOCT_MIG_FV3;
+  static constexpr bool FV3 = !MIG;
   double krow[KROW ? NNP : 1];
   const AS_LDS double* bv;
   int lane, slot, lc, gid, nct;
@@ -1087,17 +1060,15 @@ struct Chain {
   // V_CA (there is no helper wave, so the next prior part is written only after the
   // bookkeeping), the end-updated p in V_CUR_G (where spec_weight reads it anyway).  No
   // LDS is added: the tile's LDS carve decides how many chains fit (G = 4 at depth 12).
-  static constexpr bool KLDS = MIG && !FITOCT_MIG_KREG;
+  static constexpr bool KLDS = MIG;
   V k_q, k_pe, k_g;
   // (its lp / sum r^2 stay in Sp->cur_lp / cur_s2 until the bookkeeping)
   int k_dirn, k_dn, k_jn;
   uint32_t k_t;
-  // the helper publishes the booked leaf's weight by writing request numbers here
-  volatile AS_LDS int* help_wdone = nullptr;
-  int help_want = 0;
-  // deep speculation (tiles of one chain): the helper books leaf k (deep_book) while this
-  // wave completes gradient k + 1; this wave waits for booking k (book_done >= book_want)
-  // only before it stages leaf k + 2, and reads its outcome from book_res
+  // deep speculation (tiles of one or two chains, helped): the helper books leaf k
+  // (deep_book) while this wave completes gradient k + 1; this wave waits for booking k
+  // (book_done >= book_want) only before it stages leaf k + 2, and reads its outcome from
+  // book_res
   bool deep = false;
   AS_LDS double* HX = nullptr;
   volatile AS_LDS int* book_done = nullptr;
@@ -1108,7 +1079,7 @@ struct Chain {
   // Compiled where it can run: tiles of one chain (deep speculation, spare waves from the
   // start), and migrating tiles in the launch's tail (a chain alone in its tile, with two
   // idle receivers recruited as producers: kernel and receive_chain, P.tail_bidi)
-  static constexpr bool kTwoEnded = SPEC && FITOCT_DEEP_SPEC;
+  static constexpr bool kTwoEnded = SPEC;
   bool bidi = false;
   volatile AS_LDS int* bd = nullptr;
   RngKey key;
@@ -1121,7 +1092,7 @@ struct Chain {
     gid = Pr().chain_offset + lc;
     // tiles of G <= 2 chains: NUTS wave G + c helps chain slot c (tile of one chain: wave 1)
     helped = SPEC && !MIG && P_.G <= 2;
-    deep = FITOCT_DEEP_SPEC && helped;
+    deep = helped;
     HX = L.hx(L.G <= 2 ? slot_ : 0);   // (two-ended: L.G = 3, one ring extension)
     bidi = kTwoEnded && !MIG && deep && P_.bidi != 0;
     key = make_key(Pr().seed, (uint32_t)gid);
@@ -1938,7 +1909,7 @@ struct Chain {
   // the bookkeeping of the speculated leaf, while its successor is being swept
   __device__ int act_spec_book() {
     FITOCT_MARK(act_spec_book);
-    if (!helped) spec_weight();   // no helper wave in a tile of several chains
+    spec_weight();   // (act_spec_book runs only without a helper wave: tiles of several chains)
     const int r = KLDS ? leaf_book_split(ld(V_PG), ld(V_CUR_G), ld(V_CA), ld(V_MINV), Sp->cur_lp,
                                          Sp->cur_s2)
                        : leaf_book_split(k_q, k_pe, k_g, ld(V_MINV), Sp->cur_lp, Sp->cur_s2);
@@ -1957,7 +1928,7 @@ struct Chain {
       Sp->lf_e = k_dirn ? Sp->eps_used : -Sp->eps_used;
     }
     // without a helper, the next position's prior part follows the bookkeeping here
-    if (!helped && r != LB_END) prior_and_uniforms(true, k_dn, k_jn, k_t);
+    if (r != LB_END) prior_and_uniforms(true, k_dn, k_jn, k_t);
     return r == LB_END ? A_SPEC_DISCARD : A_SPEC_WAIT;
   }
 
@@ -2038,13 +2009,13 @@ struct Chain {
                   : HX + (s * (rb - ra) + (m - ra)) * Pr().bidi_rec;
   }
   // a migrating tile's chain, at the start of a transition (depth 0): two-ended when the tile
-  // hosts at most P.tail_live live chains, two idle receivers of the tile have become
+  // hosts one live chain, two idle receivers of the tile have become
   // producers and no other chain of the tile is growing a tree with them (TW_BUSY, claimed
   // by tail_claim, released when the tree is booked)
   __device__ __forceinline__ bool tail_ready() const {
     const int lv = uni(__atomic_load_n(live, __ATOMIC_RELAXED));
-    return Pr().tail_bidi != 0 && uni(Sp->depth) == 0 && uni(bd[TW_JOIN]) >= 2 && lv >= 1 &&
-           lv <= Pr().tail_live && uni(bd[TW_BUSY]) == 0;
+    return Pr().tail_bidi != 0 && uni(Sp->depth) == 0 && uni(bd[TW_JOIN]) >= 2 && lv == 1 &&
+           uni(bd[TW_BUSY]) == 0;
   }
   __device__ __forceinline__ bool tail_claim() const {
     int ok = 0;
@@ -2054,9 +2025,12 @@ struct Chain {
   // Book every leaf of transition g in Stan's tree order from the producers' rings: the
   // helper wave of a tile of one chain, or a migrating tile's chain itself.  LB_END, with
   // the status ERR_TIMEOUT if a producer's record never came (a fault)
+  // profiling build: the booking wave's cycles waiting for records / booking, leaves booked
+  long long pf_wait = 0, pf_busy = 0, pf_n = 0;
   __device__ int bidi_book_tree(const int g) {
     int cons0 = 0, cons1 = 0;
     for (;;) {
+      const long long pt0 = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
       const int s = uni(Sp->dir);   // the subtree being booked grows this end
       const int n = s ? cons1 : cons0;
       bool lost = false;
@@ -2075,11 +2049,17 @@ struct Chain {
         return LB_END;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the record after its count
+      const long long pt1 = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
       const int r = bidi_book(s, n);
       if (s) ++cons1;
       else ++cons0;
       wave_publish();
       if (lane == 0) bd[BD_CONS + s] = n + 1;
+      if (kProfile) {
+        pf_wait += pt1 - pt0;
+        pf_busy += (long long)__builtin_amdgcn_s_memtime() - pt1;
+        ++pf_n;
+      }
       if (r == LB_END) return LB_END;
     }
   }
@@ -2256,18 +2236,7 @@ struct Chain {
       persist = crit3(far, p, rtot, far, Tpb, rx, near, p, ry, minv);
     }
     sub(2, ts);
-    // phase B: the helper's weight of this leaf (or this wave's own, act_spec_book)
-    if (helped && !deep) {
-      Patience w;
-      while (*help_wdone < help_want) {
-        if (w.expired(LEAF_WAIT_TICKS)) {
-          Sp->status = ERR_TIMEOUT;
-          return LB_END;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      wave_fence();
-    }
+    // phase B: the leaf's weight (book_leaf's, or this wave's own: act_spec_book)
     const double h = Sp->spec_h, wl = H0 - h;
     const XF wleaf{Sp->spec_wm, uni(Sp->spec_we)};
     Sp->sum_metro = sum_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
@@ -2417,8 +2386,7 @@ struct Chain {
   // lines are rewritten at every other leaf (config 3: L2->memory writes 6.6x the draws
   // with ordinary stores, profiles/r03_pmc_traffic_config3.json).
   static __device__ __forceinline__ void st_draw(AS_GLB double* p, double v) {
-    if constexpr (FITOCT_NT_DRAWS) __builtin_nontemporal_store(v, p);
-    else *p = v;
+    __builtin_nontemporal_store(v, p);
   }
   __device__ void write_draw(double accept, double energy) const {
     const int t = Sp->t, W = Pr().warmup;
@@ -2700,21 +2668,6 @@ __device__ __forceinline__ unsigned long long lds_load64(const unsigned long lon
   return __atomic_load_n(p, __ATOMIC_RELAXED);
 }
 constexpr int RINGN = 16;                 // hand-off ring: >= 2 * GMAX entries
-#ifndef FITOCT_NUTS_POLL
-#define FITOCT_NUTS_POLL 1
-#endif
-#ifndef FITOCT_NUTS_WAIT_PRIO
-#define FITOCT_NUTS_WAIT_PRIO 0
-#endif
-// one-chain tiles with deep speculation (A/B knobs, -1 = the NUTS priority): the chain
-// wave's priority while it computes the next prior part during the sweep, and the helper
-// wave's -- each shares its SIMD with a gradient wave of that sweep
-#ifndef FITOCT_DEEP_PRIOR_PRIO
-#define FITOCT_DEEP_PRIOR_PRIO -1
-#endif
-#ifndef FITOCT_HELPER_PRIO
-#define FITOCT_HELPER_PRIO -1
-#endif
 
 // Migration receiver: post NUTS slot c of this tile as free and wait until a
 // crowded tile hands a chain over (returns its chain index, image loaded into
@@ -2749,7 +2702,7 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane, volatil
     const int done = __builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_DONE]));
     if (done >= P.chains) return -1;
     const int lv = __builtin_amdgcn_readfirstlane(*(volatile const AS_LDS int*)live);
-    if (P.tail_bidi && P.chains - done <= P.tail_left && lv >= 1 && lv <= P.tail_live &&
+    if (P.tail_bidi && P.chains - done <= P.tail_left && lv == 1 &&
         __builtin_amdgcn_readfirstlane(bd[TW_CLAIM]) != 3) {
       int r = -1;
       if (lane == 0) {
@@ -2770,32 +2723,7 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane, volatil
       r = __builtin_amdgcn_readfirstlane(__shfl(r, 0));
       if (r >= 0) return -2 - r;
     }
-    // (P.tail_protect) the tile's lone chain has its two producers: a migrant here would end
-    // its two-ended trees, so this receiver withdraws its post while the chain is alone, and
-    // posts again once the chain has finished
-    if (P.tail_protect && P.tail_bidi && lv == 1 &&
-        __builtin_amdgcn_readfirstlane(bd[TW_CLAIM]) == 3) {
-      int still = 0;
-      if (lane == 0) {
-        still = (g_and(&M.fmask[me], ~(1 << c)) >> c) & 1;
-        if (still) g_add(&M.hdr[MIG_WAITING], -1);
-      }
-      if (__builtin_amdgcn_readfirstlane(__shfl(still, 0))) {
-        for (;;) {
-          if (__builtin_amdgcn_readfirstlane(g_load(&M.hdr[MIG_DONE])) >= P.chains) return -1;
-          if (__builtin_amdgcn_readfirstlane(*(volatile const AS_LDS int*)live) != 1) break;
-          __builtin_amdgcn_s_sleep(64);
-        }
-        if (lane == 0) {
-          g_or(&M.fmask[me], 1 << c);
-          g_add(&M.hdr[MIG_WAITING], 1);
-        }
-        t0 = __builtin_amdgcn_s_memrealtime();
-        continue;
-      }
-      // else a donor claimed the slot first: its chain arrives in the mailbox
-    }
-    if (__builtin_amdgcn_s_memrealtime() - t0 > MIG_WAIT_TICKS) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > MIG_WAIT_TICKS) {
       int still = 0;   // withdraw the post unless a donor already claimed it
       if (lane == 0) {
         still = (g_and(&M.fmask[me], ~(1 << c)) >> c) & 1;
@@ -2830,16 +2758,28 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane, volatil
 // parameter blocks, one per problem, and tile_map[2*tile] = {problem, first
 // chain} places each tile; a tile never mixes problems, so every tile still
 // keeps one problem's bins in registers.  tile_map == nullptr: one problem.
+//
+// Paired tiles (P.pair, one-chain tiles with two-ended trajectories, 2 x tiles <= CUs): block
+// b is tile (b / 16) * 8 + b % 8 in the role (b / 8) % 2 -- 0: the primary, which hosts the
+// chain, its helper and the backward end's producer; 1: its partner, which grows the forward
+// end on its own gradient waves.  Blocks b and b + 8 (one XCD when blocks are dealt round-robin
+// over the 8 XCDs; for speed only, the hand-off is correct on any placement) form a pair.
 template <class R, int BPT, int NNP, int PPL, int MODE, int FAM, bool MIG, bool SPEC>
 __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict__ Pg,
                                                       const int* __restrict__ tile_map) {
+  int tix = blockIdx.x, role = 0;
+  if (SPEC && !MIG && ((KPc*)Pg)->pair) {   // (Pg[0]: every problem of a batch pairs alike)
+    role = (tix >> 3) & 1;
+    tix = ((tix >> 4) << 3) | (tix & 7);
+    if (tix >= ((KPc*)Pg)->pair_tiles) return;   // the grid's padding to whole groups of 16
+  }
   int pidx = 0, c0;
   if (tile_map) {
     const AS_CST int* tm = (const AS_CST int*)tile_map;
-    pidx = __builtin_amdgcn_readfirstlane(tm[2 * blockIdx.x]);
-    c0 = __builtin_amdgcn_readfirstlane(tm[2 * blockIdx.x + 1]);
+    pidx = __builtin_amdgcn_readfirstlane(tm[2 * tix]);
+    c0 = __builtin_amdgcn_readfirstlane(tm[2 * tix + 1]);
   } else {
-    c0 = blockIdx.x * ((KPc*)Pg)->G;
+    c0 = tix * ((KPc*)Pg)->G;
   }
   KPc& P = *((KPc*)Pg + pidx);   // device-resident parameter block: uniform s_load reads
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2857,23 +2797,57 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   // a request for the bookkeeping of its leaf (deep: the leaf in HX[c]) or the prior part of
   // a speculated position; its helper wave (NUTS wave G + c) runs it and publishes the
   // request number it finished
-  __shared__ int help_req[2], help_done[2], help_wdone[2], help_arg[2][3], help_res[2];
+  __shared__ int help_req[2], help_done[2], help_res[2];
   const bool spec = SPEC;
   const bool helped = SPEC && !MIG && P.G <= 2;   // spare NUTS waves help the tile's chains
   const bool bidi = Chain<PPL, NNP, FAM, MIG, SPEC>::kTwoEnded && helped &&
                    P.bidi != 0;   // ... and two producer waves
   __shared__ int live_chains;   // chains the tile hosts (speculation policy, Chain::live)
+  // paired tiles: this pair's hand-off words and buffer; pair_on: the partner has joined
+  // (partner tile: 1 = it grows the forward end, 0 = it leaves at once)
+  const bool paired = SPEC && !MIG && bidi && P.pair != 0;
+  AS_GLB int* const xh = paired ? (AS_GLB int*)P.pair_hdr + (size_t)tix * PAIR_HDR_INTS : nullptr;
+  AS_GLB double* const xb = paired ? (AS_GLB double*)P.pair_buf + (size_t)tix * P.pair_stride : nullptr;
+  __shared__ int pair_on;
 
   load_kinv<PPL, NNP>(P, L, tid);
   if (tid == 0) {
     q_reserve = 0;
     n_active = nct;
     live_chains = nct;
+    pair_on = 0;
+    if (paired && role == 0 && nct > 0) __hip_atomic_fetch_or(xh + PH_STATE, PS_START, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+    if (paired && role == 1) {
+      // join once the primary has begun; give up (LOCAL) if it has not within PAIR_JOIN_TICKS
+      // (the blocks of a launch start within a microsecond of each other on an idle chip; the
+      // primary decides only at its chain's first transition, many gradients later)
+      bool join = false;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (int st = x_ldi(xh + PH_STATE); !P.pair_test_absent;) {
+        if (st & PS_LOCAL) break;
+        int expect = st & PS_START ? st : 0;
+        const int want = st & PS_START ? st | PS_JOIN : PS_LOCAL;
+        if (!(st & PS_START) && __builtin_amdgcn_s_memrealtime() - t0 < PAIR_JOIN_TICKS) {
+          __builtin_amdgcn_s_sleep(2);
+          st = x_ldi(xh + PH_STATE);
+          continue;
+        }
+        if (__hip_atomic_compare_exchange_strong(xh + PH_STATE, &expect, want, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          join = (want & PS_JOIN) != 0;
+          break;
+        }
+        st = expect;   // the primary began (or decided) meanwhile: look again
+      }
+      if (!join) __hip_atomic_fetch_or(xh + PH_STATE, PS_LOCAL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pair_on = join ? 1 : 0;
+      n_active = join ? 1 : 0;   // the partner's bridge wave ends its gradient waves
+    }
   }
   if (tid < 2) {
     help_req[tid] = 0;
     help_done[tid] = 0;
-    help_wdone[tid] = 0;
     help_res[tid] = 0;
   }
   if (tid < GMAX) {
@@ -2889,15 +2863,15 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     if (tid == 0) {
       const MigView M(P.mig, P.mig_tiles);
       n_active = P.G;
-      __hip_atomic_store((int*)&M.load[blockIdx.x], nct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((int*)&M.load[tix], nct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add((int*)&M.hdr[MIG_STARTED], 1, __ATOMIC_RELAXED,   // a count: no data
                              __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
 
-  const bool stamp = kProfile && (P.stamps != nullptr) && lane == 0 && (wave == 0 || wave == NGW);
-  const bool wstamp = kProfile && (P.stamps != nullptr) && lane == 0 && wave < NGW;
+  const bool stamp = kProfile && (P.stamps != nullptr) && role == 0 && lane == 0 && (wave == 0 || wave == NGW);
+  const bool wstamp = kProfile && (P.stamps != nullptr) && role == 0 && lane == 0 && wave < NGW;
   long long t_wbusy = 0;
   long long t_busy = 0, n_items = 0, t_wait = 0, t_enq = 0, t_sweep = 0, t_notice = 0;
   long long t_st0 = 0, t_st1 = 0;
@@ -2938,7 +2912,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           stop = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(FITOCT_GRAD_SLEEP);
+        __builtin_amdgcn_s_sleep(1);
       }
       if (stop) break;
       const int c = (int)(e & 0xFF);
@@ -2971,8 +2945,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         ++n_items;
       }
     }
-    if (kProfile && wave == 0 && lane == 0 && P.stamps != nullptr) {
-      AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)blockIdx.x * NSTAMP;
+    if (kProfile && role == 0 && wave == 0 && lane == 0 && P.stamps != nullptr) {
+      AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)tix * NSTAMP;
       // (the interval after the last entry: the tile's live count now, normally 0 -- a
       // tile whose chains have finished waits for migrants, or the launch's end)
       occ_t[min(max(lds_load(&live_chains), 0), GMAX)] +=
@@ -2985,12 +2959,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   } else {           // ------------------------- NUTS waves
     // the sampler is the latency-critical stage and shares each SIMD with two
     // throughput-bound gradient waves: let it win issue arbitration
-    switch (P.nuts_prio) {   // s_setprio takes an immediate
-      case 0: break;
-      case 1: __builtin_amdgcn_s_setprio(1); break;
-      case 2: __builtin_amdgcn_s_setprio(2); break;
-      default: __builtin_amdgcn_s_setprio(3); break;
-    }
+    // (priority 2 / 1 / 0: -0.3 % / +-0 / -23 % on config 3)
+    __builtin_amdgcn_s_setprio(3);
     const int c = wave - NGW;
     const bool mig = MIG && P.mig != nullptr;
     using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
@@ -2998,7 +2968,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     // slot `slot` (its chain area holds the end's state; its ring of leaf records sits in the
     // area's tree levels and, in a tile of one chain, behind the chain areas).  For every
     // transition g the chain starts (BD_GEN), it leapfrogs this end from the start through
-    // the doublings drawn in direction s, at most FITOCT_BIDI_LOOK doublings past the one
+    // the doublings drawn in direction s, at most BIDI_LOOK doublings past the one
     // being booked and a ring ahead of the booking, and publishes each leaf's record.
     // `epoch`: the slot's sweeps so far (grad_cnt[slot] counts NGW per sweep).  Ends with
     // BD_GEN < 0 (the tile's chain finished) or, in a migrating tile, with the launch.
@@ -3007,6 +2977,9 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       pr.bd = (volatile AS_LDS int*)bd;
       int seen = 0;
       bool quit = false;
+      // profiling build: cycles waiting for sweeps, for the lookahead / ring room, leaves,
+      // and cycles inside trees
+      long long pf_sw = 0, pf_may = 0, pf_n = 0, pf_tree = 0;
       while (!quit) {
         int g;
         {
@@ -3051,21 +3024,29 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         wave_fence();
         if (lds_load(&bd[BD_GEN]) != g) continue;   // the start was rewritten while read
         const double e = s ? eps : -eps;
-        // may leaf n of this end grow now: within FITOCT_BIDI_LOOK doublings of the booked one,
+        // may leaf n of this end grow now: within BIDI_LOOK doublings of the booked one,
         // and the ring.  Once true it stays true for the transition (the booked depth and the
         // helper's count only grow), so a check made while a sweep runs holds after it
         auto may = [&](const int n) -> bool {
-          const int dl = min(pr.uni(*(volatile const AS_LDS int*)&S0.depth) + FITOCT_BIDI_LOOK,
+          const int dl = min(pr.uni(*(volatile const AS_LDS int*)&S0.depth) + BIDI_LOOK,
                              P.max_depth - 1);
           const int lim = pr.uni(__shfl(cum, dl));
           const int cons = lds_load(&bd[BD_CONS + s]);
           return n < lim && n - cons < P.bidi_rb;
         };
+        const long long pft0 = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
         auto wait_may = [&](const int n) -> bool {   // false: the tree ended
           Patience w;
+          const long long pt = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
           for (;;) {
-            if (lds_load(&bd[BD_GEN]) != g) return false;
-            if (may(n)) return true;
+            if (lds_load(&bd[BD_GEN]) != g) {
+              if (kProfile) pf_may += (long long)__builtin_amdgcn_s_memtime() - pt;
+              return false;
+            }
+            if (may(n)) {
+              if (kProfile) pf_may += (long long)__builtin_amdgcn_s_memtime() - pt;
+              return true;
+            }
             // the other end may grow for long (deep trees, large N).  In effect this wait
             // ends with BD_GEN: its bound outlasts the bound on the whole tree (MIG_WAIT_TICKS
             // from the tree's start), after which BD_GEN changes
@@ -3099,15 +3080,20 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         for (int n = 0;; ++n) {
           // (a migrating launch's tail keeps the record-first order: config 3 measured -1.3 %
           // with the successor staged first, config 2 +13.7 %; profiles/r05_ab_stage.txt)
-          const bool pre = (!MIG || FITOCT_MIG_STAGE_FIRST) && may(n + 1);
+          const bool pre = !MIG && may(n + 1);
           bool late = false;
           Patience ws;
+          const long long pt = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
           while (lds_load(&grad_cnt[slot]) < (int)(NGW * epoch)) {
             if (ws.expired(LEAF_WAIT_TICKS)) {
               late = true;
               break;
             }
-            __builtin_amdgcn_s_sleep(FITOCT_PROD_SLEEP);
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (kProfile) {
+            pf_sw += (long long)__builtin_amdgcn_s_memtime() - pt;
+            ++pf_n;
           }
           if (late) {
             quit = true;
@@ -3149,16 +3135,214 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           }
           pr.prior_part();
         }
+        if (kProfile) pf_tree += (long long)__builtin_amdgcn_s_memtime() - pft0;
+      }
+      if (kProfile && P.stamps != nullptr && lane == 0) {   // this end's producer (either tile)
+        AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)tix * NSTAMP + 88 + 4 * s;
+        o[0] = pf_sw;
+        o[1] = pf_may;
+        o[2] = pf_n;
+        o[3] = pf_tree;
       }
     };
-    if (bidi && c == 1) {   // two-ended trajectories: book every leaf in tree order
+    // ---- paired tiles (P.pair): the bridge waves.  The forward end's producer runs unchanged
+    // in the partner tile (NUTS wave 3, chain area 2, its own ring in LDS); two bridge waves make
+    // the pair look like one tile to it and to the primary's helper:
+    //   bridge_in (primary, NUTS wave 3, where that producer would run): each transition's start
+    //     (producer area 2, written by bidi_begin) and the helper's progress on the forward end
+    //     (booked leaves, booked depth) out to the pair's words; the partner's leaf records in
+    //     from the pair's ring into the primary's forward ring, published as a local producer
+    //     would (BD_PROD + 1);
+    //   bridge_out (partner, NUTS wave 2): the start into the producer's area and BD_GEN; the
+    //     helper's progress into BD_CONS + 1 and the depth the producer's lookahead reads; the
+    //     producer's records out to the pair's ring, then PH_COUNT.
+    // Every record reaches the helper only through both bridges, and the producer may overwrite
+    // ring slot n % rb only once the helper has booked leaf n (its ring-room check reads the
+    // mirrored, never larger, booked count), so one flow count guards all three rings.  Counts
+    // and the booked depth carry their transition (gen << 16) and only grow within it.
+    // the forward end's producer area (NUTS slot 2) and its ring (Chain::brec(1, n))
+    auto fwd_rec = [&](const int n) -> AS_LDS double* {
+      const int rb = P.bidi_rb, ra = P.bidi_rba, m = n % rb;
+      return m < ra ? L.lvls(2) + m * P.bidi_rec : L.hx(0) + ((rb - ra) + (m - ra)) * P.bidi_rec;
+    };
+    auto pair_start = [&]() { return xb; };
+    auto pair_ring = [&]() { return xb + 4 * Ch::VLEN + PAIR_START_DOUBLES; };
+    auto bridge_in = [&]() -> bool {   // false: the pair did not form (grow the end here)
+      {
+        Patience w;   // the chain's first transition (or its end)
+        while (lds_load(&bd[BD_GEN]) == 0 && !w.expired(MIG_WAIT_TICKS)) __builtin_amdgcn_s_sleep(1);
+      }
+      int st = 0;
+      if (lane == 0) {
+        int expect = PS_START;
+        st = __hip_atomic_compare_exchange_strong(xh + PH_STATE, &expect, PS_START | PS_LOCAL,
+                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                 ? PS_START | PS_LOCAL
+                 : expect;
+      }
+      st = __builtin_amdgcn_readfirstlane(__shfl(st, 0));
+      if ((st & PS_LOCAL) || !(st & PS_JOIN)) return false;
+      constexpr int VL = Ch::VLEN;
+      const int nrec = 3 * P.D + 2, rb = P.bidi_rb, rec = P.bidi_rec;
+      AS_GLB double* const xs = pair_start();
+      AS_GLB double* const xr0 = pair_ring();
+      const volatile AS_LDS int* depth = (const volatile AS_LDS int*)&L.cs(0).depth;
+      int seen = 0, copied = 0, last_cons = -1, last_depth = -1;
+      Patience idle;
+      for (;;) {
+        const int g = lds_load(&bd[BD_GEN]);
+        if (g != seen) {
+          if (g < 0) {
+            if (lane == 0) x_sti(xh + PH_GEN, -1);
+            break;
+          }
+          wave_fence();   // the start after its number
+          const AS_LDS double* pv = L.vecs(2);
+          const AS_LDS ChainScalars* ps = &L.cs(2);
+#pragma unroll
+          for (int s = 0; s < PPL; ++s) {
+            const int k = s * WAVE + lane;
+            x_st(xs + k, pv[V_E0_Q * VL + k]);
+            x_st(xs + VL + k, pv[V_E0_P * VL + k]);
+            x_st(xs + 2 * VL + k, pv[V_E0_G * VL + k]);
+            x_st(xs + 3 * VL + k, pv[V_MINV * VL + k]);
+          }
+          if (lane == 0) {
+            x_st(xs + 4 * VL, ps->eps_used);
+            x_st(xs + 4 * VL + 1, ps->end_lp[0]);
+            x_st(xs + 4 * VL + 2, ps->end_s2[0]);
+            x_sti(xh + PH_T, ps->t);
+            x_sti(xh + PH_LC, lds_load(&bd[TW_LC]));
+          }
+          x_drain();   // the start has reached memory before its number
+          if (lane == 0) {
+            x_sti(xh + PH_GEN, g);
+            atomicAdd(P.pair_count, 1ULL);
+          }
+          seen = g;
+          copied = 0;
+          last_cons = last_depth = -1;
+          idle = Patience{};
+          continue;
+        }
+        // the helper's progress on the forward end, for the partner's lookahead and ring room
+        const int cons = lds_load(&bd[BD_CONS + 1]);
+        const int dep = *depth;
+        if (lds_load(&bd[BD_GEN]) == seen) {
+          if (lane == 0 && cons != last_cons) x_sti(xh + PH_CONS, (seen << 16) | cons);
+          if (lane == 0 && dep != last_depth) x_sti(xh + PH_DEPTH, (seen << 16) | dep);
+          last_cons = cons;
+          last_depth = dep;
+        }
+        // the partner's records of this transition
+        const int pc = __builtin_amdgcn_readfirstlane(x_ldi(xh + PH_COUNT));
+        if ((pc >> 16) == seen && (pc & 0xFFFF) > copied) {
+          const int cnt = pc & 0xFFFF;
+          for (int n = copied; n < cnt; ++n) {
+            const AS_GLB double* src = xr0 + (size_t)(n % rb) * rec;
+            AS_LDS double* dst = fwd_rec(n);
+            for (int i = lane; i < nrec; i += WAVE) dst[i] = x_ld(src + i);
+          }
+          wave_publish();   // the records land before their count
+          if (lane == 0) __atomic_store_n(&bd[BD_PROD + 1], (seen << 16) | cnt, __ATOMIC_RELAXED);
+          copied = cnt;
+          idle = Patience{};
+          continue;
+        }
+        if (idle.expired(2 * MIG_WAIT_TICKS)) break;   // never, short of a fault
+        __builtin_amdgcn_s_sleep(1);
+      }
+      return true;
+    };
+    auto bridge_out = [&]() {
+      constexpr int VL = Ch::VLEN;
+      const int nrec = 3 * P.D + 2, rb = P.bidi_rb, rec = P.bidi_rec;
+      AS_GLB double* const xs = pair_start();
+      AS_GLB double* const xr0 = pair_ring();
+      volatile AS_LDS int* depth = (volatile AS_LDS int*)&L.cs(0).depth;   // the producer's S0
+      if (lane == 0) {
+        bd[TW_CHAIN] = 0;
+        *depth = 0;
+      }
+      int seen = 0, copied = 0;
+      Patience idle;
+      for (;;) {
+        const int g = __builtin_amdgcn_readfirstlane(x_ldi(xh + PH_GEN));
+        const int cw = __builtin_amdgcn_readfirstlane(x_ldi(xh + PH_CONS));
+        const int dw = __builtin_amdgcn_readfirstlane(x_ldi(xh + PH_DEPTH));
+        if (g != seen) {
+          if (g < 0) break;
+          AS_LDS double* pv = L.vecs(2);
+          AS_LDS ChainScalars* ps = &L.cs(2);
+#pragma unroll
+          for (int s = 0; s < PPL; ++s) {
+            const int k = s * WAVE + lane;
+            pv[V_E0_Q * VL + k] = x_ld(xs + k);
+            pv[V_E0_P * VL + k] = x_ld(xs + VL + k);
+            pv[V_E0_G * VL + k] = x_ld(xs + 2 * VL + k);
+            pv[V_MINV * VL + k] = x_ld(xs + 3 * VL + k);
+          }
+          if (lane == 0) {
+            ps->eps_used = x_ld(xs + 4 * VL);
+            ps->end_lp[0] = x_ld(xs + 4 * VL + 1);
+            ps->end_s2[0] = x_ld(xs + 4 * VL + 2);
+            ps->t = x_ldi(xh + PH_T);
+            bd[TW_LC] = x_ldi(xh + PH_LC);
+            bd[BD_CONS + 1] = 0;
+            *depth = 0;
+          }
+          wave_publish();   // the start lands before the transition's number
+          if (lane == 0) __atomic_store_n(&bd[BD_GEN], g, __ATOMIC_RELAXED);
+          seen = g;
+          copied = 0;
+          idle = Patience{};
+          continue;
+        }
+        if (lane == 0) {   // the helper's progress: never lowered within the transition
+          if ((cw >> 16) == seen && (cw & 0xFFFF) > bd[BD_CONS + 1]) bd[BD_CONS + 1] = cw & 0xFFFF;
+          if ((dw >> 16) == seen && (dw & 0xFFFF) > *depth) *depth = dw & 0xFFFF;
+        }
+        const int pw = lds_load(&bd[BD_PROD + 1]);
+        if ((pw >> 16) == seen && (pw & 0xFFFF) > copied) {
+          const int cnt = pw & 0xFFFF;
+          wave_fence();   // the records after their count
+          for (int n = copied; n < cnt; ++n) {
+            const AS_LDS double* src = fwd_rec(n);
+            AS_GLB double* dst = xr0 + (size_t)(n % rb) * rec;
+            for (int i = lane; i < nrec; i += WAVE) x_st(dst + i, src[i]);
+          }
+          x_drain();   // every record has reached memory before the count
+          if (lane == 0) x_sti(xh + PH_COUNT, (seen << 16) | cnt);
+          copied = cnt;
+          idle = Patience{};
+          continue;
+        }
+        if (idle.expired(2 * MIG_WAIT_TICKS)) break;   // never, short of a fault
+        __builtin_amdgcn_s_sleep(1);
+      }
+      // the chain has finished: stop the producer, let it drain its sweep, end the tile
+      if (lane == 0) __atomic_store_n(&bd[BD_GEN], -1, __ATOMIC_RELAXED);
+      {
+        Patience w;
+        while (lds_load(&bd[BD_EXIT]) < 1 && !w.expired(LEAF_WAIT_TICKS)) __builtin_amdgcn_s_sleep(1);
+      }
+      wave_fence();
+      if (lane == 0) atomicSub(&n_active, 1);
+    };
+    if constexpr (SPEC && !MIG) {
+      if (role == 1 && pair_on && c == 2) bridge_out();   // partner tile: the bridge
+    }
+    if (bidi && role == 0 && c == 1) {   // two-ended trajectories: book every leaf in tree order
       Ch ch(P, L, 0, c0, lane, nct);
       ch.bd = (volatile AS_LDS int*)bd;
       int seen = 0;
+      long long pf_idle = 0;
       for (;;) {
         int g;
         Patience w;   // (init and step-size searches run between transitions)
         bool quit = false;
+        const long long pt0 = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
         while ((g = lds_load(&bd[BD_GEN])) == seen) {   // the next transition, or the end
           if (w.expired(MIG_WAIT_TICKS)) {
             quit = true;
@@ -3166,6 +3350,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           }
           __builtin_amdgcn_s_sleep(1);
         }
+        if (kProfile) pf_idle += (long long)__builtin_amdgcn_s_memtime() - pt0;
         if (quit || g < 0) break;
         seen = g;
         wave_fence();   // the transition's start state is read after its number
@@ -3173,14 +3358,27 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         wave_publish();   // the booking's LDS writes land before the end is published
         if (lane == 0) __atomic_store_n(&bd[BD_END], g, __ATOMIC_RELAXED);
       }
+      if (kProfile && P.stamps != nullptr && lane == 0) {   // the booking wave's time
+        AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)tix * NSTAMP;
+        o[84] = ch.pf_busy;
+        o[85] = ch.pf_wait;
+        o[86] = ch.pf_n;
+        o[87] = pf_idle;
+      }
     }
-    if (bidi && c >= 2) {   // two-ended trajectories: producer of the backward (c = 2) / forward end
-      produce(c - 2, c - 1, 0);
+    // two-ended trajectories: producer of the backward (c = 2) / forward end (c = 3); paired
+    // tiles: the forward end grows in the partner tile (its NUTS wave 3) and the primary's
+    // wave 3 is the bridge.  (One call site: produce is inlined once.)
+    if (bidi && c >= 2 && (role == 0 || (pair_on && c == 3))) {
+      bool here = true;
+      if constexpr (SPEC && !MIG) {
+        if (paired && role == 0 && c == 3) here = !bridge_in();
+      }
+      if (here) produce(c - 2, c - 1, 0);
       wave_fence();
       if (lane == 0) atomicAdd(&bd[BD_EXIT], 1);
     }
     if (helped && !bidi && c >= P.G && c - P.G < nct) {   // the helper wave of chain slot c - G
-      if (FITOCT_HELPER_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_HELPER_PRIO);
       using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
       const int hs = c - P.G;
       Ch ch(P, L, hs, c0 + hs, lane, nct);
@@ -3200,26 +3398,17 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         w = Patience{};
         seen = r;
         wave_fence();   // the request's arguments are read after its number
-        if (ch.deep) {   // book the handed-over leaf; publish its outcome, then the number
-          const int res = ch.deep_book();
+        // book the handed-over leaf; publish its outcome, then the number
+        const int res = ch.deep_book();
+        wave_publish();
+        if (lane == 0) {
+          __atomic_store_n(&help_res[hs], res, __ATOMIC_RELAXED);
           wave_publish();
-          if (lane == 0) {
-            __atomic_store_n(&help_res[hs], res, __ATOMIC_RELAXED);
-            wave_publish();
-            __atomic_store_n(&help_done[hs], seen, __ATOMIC_RELAXED);
-          }
-          continue;
+          __atomic_store_n(&help_done[hs], seen, __ATOMIC_RELAXED);
         }
-        ch.spec_weight();   // first what the chain's bookkeeping waits for
-        wave_publish();
-        if (lane == 0) __atomic_store_n(&help_wdone[hs], seen, __ATOMIC_RELAXED);
-        ch.prior_and_uniforms(true, lds_load(&help_arg[hs][0]), lds_load(&help_arg[hs][1]),
-                              (uint32_t)lds_load(&help_arg[hs][2]));
-        wave_publish();
-        if (lane == 0) __atomic_store_n(&help_done[hs], seen, __ATOMIC_RELAXED);
       }
     }
-    if (c < (mig ? P.G : nct)) {
+    if (role == 0 && c < (mig ? P.G : nct)) {
       using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
       long long epoch = 0;     // this slot's hand-offs (grad_cnt[c] counts NGW per epoch)
       int lc = c < nct ? c0 + c : -1;
@@ -3236,10 +3425,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         for (;;) {
           FITOCT_MARK(nuts_loop);
         const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
-        const bool lowp = FITOCT_DEEP_PRIOR_PRIO >= 0 && a == Ch::A_PRIOR && ch.deep;
-        if (lowp) __builtin_amdgcn_s_setprio(FITOCT_DEEP_PRIOR_PRIO);
         const int y = ch.run(a);
-        if (lowp) __builtin_amdgcn_s_setprio(3);
         if (Ch::kTwoEnded && y == Ch::A_BIDI_TREE) {   // the producers and the helper grow the tree
           const int g = lds_load(&bd[BD_GEN]);
           bool late = false;
@@ -3247,15 +3433,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             ch.bidi_book_tree(g);
           } else {
             Patience w;
-            if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_BIDI_IDLE_PRIO);
             while (lds_load(&bd[BD_END]) != g) {   // a whole tree
               if (w.expired(MIG_WAIT_TICKS)) {
                 late = true;
                 break;
               }
-              __builtin_amdgcn_s_sleep(FITOCT_BIDI_IDLE_SLEEP);
+              __builtin_amdgcn_s_sleep(1);
             }
-            if (FITOCT_BIDI_IDLE_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
           }
           if constexpr (MIG) {   // the producers stop growing this tree
             wave_publish();
@@ -3288,12 +3472,6 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             if (ch.deep) {
               wave_publish();   // the hand-off (HX) lands before the request number
               __atomic_store_n(&help_req[c], hreq + 1, __ATOMIC_RELAXED);
-            } else if (helped) {
-              help_arg[c][0] = ch.k_dn;
-              help_arg[c][1] = ch.k_jn;
-              help_arg[c][2] = (int)ch.k_t;
-              wave_publish();   // the arguments land before the request number
-              __atomic_store_n(&help_req[c], hreq + 1, __ATOMIC_RELAXED);
             }
           }
           if (stamp) t_enq = (long long)__builtin_amdgcn_s_memtime();
@@ -3307,12 +3485,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             in_sweep = true;
             continue;
           }
-          if (helped) {
-            ++hreq;
-            ch.help_wdone = (volatile AS_LDS int*)&help_wdone[c];
-            ch.help_want = hreq;
-          }
-          ++epoch;
+          ++epoch;   // (no helper wave: this wave books the leaf during the sweep)
           a = Ch::A_SPEC_BOOK;
           continue;
         }
@@ -3321,8 +3494,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           Patience w;
           const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
           if (stamp) t_busy += w0 - s0;
-          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch) ||
-                 (helped && lds_load(&help_done[c]) < hreq)) {
+          while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
             if (w.expired(LEAF_WAIT_TICKS)) {
               late = true;
               break;
@@ -3359,15 +3531,15 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           // several chains, the wait is long and the sampler is not the bottleneck: poll
           // rarely, so the waiting wave leaves the SIMD's issue to the gradient wave.
           if (P.G >= 2 && (BPT >= 8 || BPT == 0)) {
-            if (FITOCT_NUTS_WAIT_PRIO >= 0) __builtin_amdgcn_s_setprio(FITOCT_NUTS_WAIT_PRIO);
+            __builtin_amdgcn_s_setprio(0);
             while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
               if (w.expired(LEAF_WAIT_TICKS)) {
                 late = true;
                 break;
               }
-              __builtin_amdgcn_s_sleep(FITOCT_NUTS_POLL);
+              __builtin_amdgcn_s_sleep(1);
             }
-            if (FITOCT_NUTS_WAIT_PRIO >= 0) __builtin_amdgcn_s_setprio(3);
+            __builtin_amdgcn_s_setprio(3);
           } else {
             while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) {
               if (w.expired(LEAF_WAIT_TICKS)) {
@@ -3470,9 +3642,9 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       if (lane == 0) atomicSub(&n_active, 1);
     }
   }
-  if (wstamp) ((AS_GLB long long*)P.stamps)[(size_t)blockIdx.x * NSTAMP + 56 + wave] = t_wbusy;
+  if (wstamp) ((AS_GLB long long*)P.stamps)[(size_t)tix * NSTAMP + 56 + wave] = t_wbusy;
   if (stamp) {
-    AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)blockIdx.x * NSTAMP;
+    AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)tix * NSTAMP;
     if (wave == 0) {
       o[0] = n_items;
       o[1] = t_busy;

@@ -37,6 +37,10 @@ struct fitoct_plan {
   int* h_prog = nullptr;      // host-pinned [chains]: transitions done (kernel-written)
   int* h_cancel = nullptr;    // host-pinned flag polled by the kernel
   long long* d_stamps = nullptr;   // diagnostic stamps of the launch in flight
+  int* d_pair_hdr = nullptr;       // paired tiles (KParams::pair): hand-off words
+  double* d_pair_buf = nullptr;    // ... starts and rings
+  // blocks of the launch: the tiles, or with paired tiles a primary and a partner each
+  int grid() const { return kp.pair ? fitoct::pair_grid(tiles) : tiles; }
 
   // ---- multi-device plan (cfg.n_devices > 1; multi_device.cpp) ----
   // One single-device plan per device; shard r runs this plan's chains
@@ -66,6 +70,9 @@ struct fitoct_batch {
   // multi-device layer when another device's chain failed; cleared by each run
   int* h_cancel = nullptr;
   int* d_cancel = nullptr;    // its device alias
+  int* d_pair_hdr = nullptr;  // paired tiles (every problem's KParams::pair_*)
+  double* d_pair_buf = nullptr;
+  int pair_stride = 0;
 
   // ---- multi-device batch: problems [sub_off[r], sub_off[r] + subs[r]->plans.size())
   // on sub-batch r, one device each (multi_device.cpp) ----

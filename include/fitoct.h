@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FITOCT_ABI_VERSION 6
+#define FITOCT_ABI_VERSION 7
 /* largest accepted N (depth bins): bounds every host and device allocation derived from it */
 #define FITOCT_MAX_BINS (1 << 22)
 /* largest device list of one call (fitoct_config.devices) */
@@ -146,6 +146,8 @@ typedef struct fitoct_result {
   int64_t two_ended_transitions; /* out (ABI 6): transitions whose trajectory grew both ends at
                                once (tiles of one chain; chains alone in a migrating launch's
                                tail); the draws do not depend on it */
+  int64_t paired_transitions; /* out (ABI 7): of those, transitions whose forward end grew in a
+                               partner tile (fitoct_plan_info::paired); no effect on draws */
 } fitoct_result;
 
 /* Static description of a planned run. */
@@ -165,12 +167,21 @@ typedef struct fitoct_plan_info {
   int32_t n_devices;       /* devices the plan's chains (a batch's problems) run on */
   /* ABI 6: two-ended trajectories (tiles of one chain grow the trajectory's backward and
    * forward ends on two spare waves at once; same draws bit for bit).  two_ended = 1 when
-   * the plan's one-chain tiles run them; ring_records = leaf records per end's LDS ring,
+   * the plan's one-chain tiles run them, 2 (ABI 7) when a migrating plan's chains do so once
+   * alone in their tile (the launch's tail: two idle receivers of the tile become the
+   * producers), 0 when off; ring_records = leaf records per end's LDS ring,
    * ring_records_in_levels = how many of them sit in the producer's tree-level area (the
    * rest extend the LDS carve); both 0 when off. */
   int32_t two_ended;
   int32_t ring_records;
   int32_t ring_records_in_levels;
+  /* ABI 7: paired tiles.  1 when a plan of one-chain two-ended tiles that fit twice on the
+   * chip (2 x tiles <= CUs, e.g. 128 chains on 256 CUs) launches a partner tile per tile that
+   * grows the forward end on its own gradient waves (workgroups = pair_grid(tiles), see
+   * `workgroups`); same draws bit for bit.  A partner that gets no CU at launch leaves its
+   * tile to grow both ends itself (fitoct_result::paired_transitions counts the paired ones). */
+  int32_t paired;
+  int32_t workgroups;      /* workgroups launched (tiles, or 16 * ceil(tiles / 8) when paired) */
 } fitoct_plan_info;
 
 /* fitoct_plan_info::sampler.  PLAIN: no speculation, no migration;

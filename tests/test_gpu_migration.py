@@ -64,30 +64,26 @@ def _run_env(prob, cfg, **env):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("family,N,left,live,protect", [("horseshoe", 2048, None, None, None),
-                                                        ("normal", 512, None, None, None),
-                                                        ("lasso", 1024, "256", None, None),
-                                                        ("horseshoe", 2048, None, "2", None),
-                                                        ("normal", 512, "512", "2", None),
-                                                        ("horseshoe", 2048, None, None, "1")])
-def test_tail_two_ended_preserves_draws_bitwise(family, N, left, live, protect):
+@pytest.mark.parametrize("family,N,left", [("horseshoe", 2048, None),
+                                           ("normal", 512, None),
+                                           ("lasso", 1024, "256"),
+                                           ("normal", 512, "512")])
+def test_tail_two_ended_preserves_draws_bitwise(family, N, left):
     """The launch's tail (nuts_device.hip receive_chain, P.tail_bidi): once at most
     tail_left chains are unfinished (default: every chain of the launch; 256: one per
-    tile), a chain alone in its migrating tile (FITOCT_TAIL_LIVE=2: or sharing it with one
-    other chain, one of the two at a time) recruits two idle receivers of the tile as
+    tile), a chain alone in its migrating tile recruits two idle receivers of the tile as
     producers and grows both trajectory ends at once, booking the leaves itself.  Draws,
     step sizes, metrics, last positions and leapfrog counts equal those of the same launch
     without it (FITOCT_NO_TAIL_BIDI=1) and without migration at all, and the run reports
-    two-ended transitions.  FITOCT_TAIL_PROTECT=1: a tile whose lone chain has its producers
-    takes no migrant (its last receiver withdraws its post until the chain finishes)."""
+    two-ended transitions."""
     prob = _prob(family, N, 15)
     cfg = SamplerConfig(chains=1024, warmup=100, samples=100, seed=23, max_treedepth=8)
     info, a = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI=None, FITOCT_TAIL_LEFT=left,
-                       FITOCT_NO_MIGRATE=None, FITOCT_TAIL_LIVE=live, FITOCT_TAIL_PROTECT=protect)
+                       FITOCT_NO_MIGRATE=None)
     _, b = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI="1", FITOCT_TAIL_LEFT=None,
-                    FITOCT_NO_MIGRATE=None, FITOCT_TAIL_LIVE=None)
+                    FITOCT_NO_MIGRATE=None)
     _, c = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI=None, FITOCT_TAIL_LEFT=None,
-                    FITOCT_NO_MIGRATE="1", FITOCT_TAIL_LIVE=None)
+                    FITOCT_NO_MIGRATE="1")
     assert info["chains_per_tile"] == 4 and info["sampler"] == 3
     assert a.two_ended_transitions > 0, "no tail transition was two-ended"
     assert b.two_ended_transitions == 0 and c.two_ended_transitions == 0
