@@ -41,7 +41,6 @@ inline hipError_t launch(bool logp, bool mixed, int bpt, int nnp, const KParams&
   }
 }
 int lds_bytes(int ppl, int G, int max_depth);
-int lvl_doubles(int ppl, int max_depth);
 int mig_img_words(int ppl);
 }  // namespace fitoct
 
@@ -694,7 +693,8 @@ bool want_pairs(const KParams& k, int tiles, int ncu) {
 int alloc_pairs(KParams& k, int tiles, int ppl, int** hdr, double** buf) {
   k.pair = 1;
   k.pair_tiles = tiles;
-  k.pair_stride = (PAIR_START_DOUBLES + WAVE * ppl * 4 + k.bidi_rb * k.bidi_rec + 15) / 16 * 16;
+  // the start (q, p, g, minv + scalars), then one subtree record (5 vectors + 16 scalars)
+  k.pair_stride = (PAIR_START_DOUBLES + WAVE * ppl * (4 + 5) + 16 + 15) / 16 * 16;
   HIP_TRY(hipMalloc(hdr, sizeof(int) * PAIR_HDR_INTS * (size_t)tiles));
   HIP_TRY(hipMalloc(buf, sizeof(double) * (size_t)k.pair_stride * tiles));
   k.pair_hdr = *hdr;
@@ -748,7 +748,9 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   pl->draws_bytes = sizeof(double) * (size_t)C * k.iters_saved * k.ncols;
   const int vlen = WAVE * pl->ppl;
   auto setup = [&]() -> int {
-    HIP_TRY(hipMalloc(&pl->d_stack, sizeof(double) * (size_t)C * (cfg->max_treedepth + 1) * POOL_VECS * vlen));
+    // proposal pools: the chains', then the two-ended producers' (GMAX per tile; produce)
+    const size_t pools = (size_t)C + (size_t)GMAX * ((C + pl->kp.G - 1) / pl->kp.G);
+    HIP_TRY(hipMalloc(&pl->d_stack, sizeof(double) * pools * (cfg->max_treedepth + 1) * POOL_VECS * vlen));
     HIP_TRY(hipMalloc(&pl->d_fin, sizeof(double) * (size_t)C * (1 + 2 * D)));
     HIP_TRY(hipMalloc(&pl->d_status, sizeof(int) * C));
     // [chains] leapfrogs per chain, then the launch's two-ended and paired transition counts
@@ -822,46 +824,30 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
     k.spec_live = std::max(0, std::min(live, GMAX));
     k.spec = k.spec_live > 0 ? 1 : 0;
   }
-  // Two-ended trajectories (nuts_device.hip): tiles of one chain with deep speculation grow
-  // the trajectory's two ends at once on two spare NUTS waves, each into a ring of leaf
-  // records in the tile's LDS, behind two more chain areas for them.  Same draws bit for bit.
-  // Each ring fills its producer's unused tree-level area, then takes what LDS is left (at most
-  // 256 records each; off below 4).  FITOCT_NO_BIDI=1: off; FITOCT_BIDI_RB=n: at most n records.
+  // Two-ended trajectories (nuts_device.hip): tiles of one chain grow the trajectory's two
+  // ends at once -- two spare NUTS waves build the subtrees of each direction whole, each in a
+  // chain area of its own, and the chain's wave books the trajectory level from one record per
+  // subtree.  Same draws bit for bit.  The three chain areas must fit, else the tile stays on
+  // the one-ended path (at Nn 16..24 a chain area holds two parameters per lane: three of
+  // them at max_treedepth 10 take ~181 KB of the 160 KB).  FITOCT_NO_BIDI=1: off.
   k.bidi = 0;
   if (k.spec && k.G == 1 && pl->mig_bytes == 0 && getenv("FITOCT_NO_BIDI") == nullptr) {
-    const int rec = (3 * D + 2 + 1) / 2 * 2;   // doubles, 16-byte records
     const int base = lds_bytes(pl->ppl, 3, k.max_depth);
-    const int avail = 160 * 1024 - 256 - STATIC_LDS_RESERVE - base;
-    const int ra = lvl_doubles(pl->ppl, k.max_depth) / rec;
-    int rb = std::min(256, ra + (avail > 0 ? avail / (2 * rec * 8) : 0));
-    if (const char* e = getenv("FITOCT_BIDI_RB")) rb = std::min(rb, std::max(1, atoi(e)));
-    // the three chain areas alone must fit, else the tile stays on the one-ended path (at
-    // Nn 16..24 a chain area holds two parameters per lane: three of them at max_treedepth
-    // 10 take ~181 KB of the 160 KB)
-    if (avail >= 0 && (rb >= 4 || (getenv("FITOCT_BIDI_RB") && rb >= 1))) {
+    if (base <= 160 * 1024 - STATIC_LDS_RESERVE) {
       k.bidi = 1;
-      k.bidi_rb = rb;
-      k.bidi_rba = std::min(ra, rb);
-      k.bidi_rec = rec;
-      pl->lds = base + 2 * (rb - k.bidi_rba) * rec * 8;
+      pl->lds = base;
     }
   }
   // Two-ended trajectories in the tail of a migrating launch (nuts_device.hip receive_chain):
-  // the rings live in the producers' own tree-level areas (no LDS added).  Same draws bit
-  // for bit.  FITOCT_NO_TAIL_BIDI=1: off; FITOCT_TAIL_LEFT=n: start at n unfinished chains
-  // (default: every chain of the launch -- a chain alone in its tile goes two-ended whenever two
-  // receivers are idle; one per tile measured 1 % slower on config 3).
+  // the producers are idle receivers of the tile (their own chain areas: no LDS added).  Same
+  // draws bit for bit.  FITOCT_NO_TAIL_BIDI=1: off; FITOCT_TAIL_LEFT=n: start at n unfinished
+  // chains (default: every chain of the launch -- a chain alone in its tile goes two-ended
+  // whenever two receivers are idle; one per tile measured 1 % slower on config 3).
   k.tail_bidi = 0;
   if (pl->mig_bytes > 0 && k.spec && getenv("FITOCT_NO_TAIL_BIDI") == nullptr) {
-    const int rec = (3 * D + 2 + 1) / 2 * 2;
-    const int ra = std::min(256, lvl_doubles(pl->ppl, k.max_depth) / rec);
-    if (ra >= 4) {
-      k.tail_bidi = 1;
-      k.bidi_rb = k.bidi_rba = ra;
-      k.bidi_rec = rec;
-      k.tail_left = k.chains;   // from the start (config 3: +1.0 % over one per tile, profiles/r05_ab_tail_left.txt)
-      if (const char* e = getenv("FITOCT_TAIL_LEFT")) k.tail_left = std::max(0, atoi(e));
-    }
+    k.tail_bidi = 1;
+    k.tail_left = k.chains;   // from the start (config 3: +1.0 % over one per tile, profiles/r05_ab_tail_left.txt)
+    if (const char* e = getenv("FITOCT_TAIL_LEFT")) k.tail_left = std::max(0, atoi(e));
   }
   // (a batch pairs its tiles itself: fitoct_batch_create)
   if (g_chains == 0 && want_pairs(k, pl->tiles, pl->ncu)) {
@@ -896,8 +882,8 @@ int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
     info->draws_bytes = (int64_t)pl->draws_bytes;
     const bool te = pl->kp.bidi || pl->kp.tail_bidi;
     info->two_ended = pl->kp.bidi ? 1 : pl->kp.tail_bidi ? 2 : 0;
-    info->ring_records = te ? pl->kp.bidi_rb : 0;
-    info->ring_records_in_levels = te ? pl->kp.bidi_rba : 0;
+    info->ring_records = te ? 1 : 0;   // (ABI 7: one subtree record per end)
+    info->ring_records_in_levels = 0;
     info->paired = pl->kp.pair;
     info->workgroups = pl->grid();
     return FITOCT_OK;

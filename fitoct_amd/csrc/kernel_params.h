@@ -119,19 +119,14 @@ struct KParams {
   double* s2_out;           // [points]
   // appended (ABI 5), so the offsets of every field above are those of round 3
   double theta_rate;        // mono-exp, theta_prior = 1: theta_k ~ exponential(theta_rate)
-  // ---- two-ended trajectories (tiles of one chain with deep speculation; 0: off) ----
-  // two producer waves leapfrog the trajectory's backward and forward ends from the
-  // transition's start at once, each into a ring of leaf records; the helper wave books the
-  // leaves in Stan's tree order (nuts_device.hip, "Two-ended trajectories")
+  // ---- two-ended trajectories (tiles of one chain; 0: off) ----
+  // two producer waves build the subtrees of the trajectory's backward and forward ends from
+  // the transition's start at once, each in its own chain area; the chain's wave books the
+  // trajectory level from one record per subtree (nuts_device.hip, "two-ended trajectories")
   int bidi;                 // 1: on (the tile's LDS then carves 3 chain areas)
-  int bidi_rb;              // leaf records per ring (two rings in LDS after the chain areas)
-  int bidi_rec;             // doubles per record: q, end-updated p, g (D each), lp, sum r^2
-  int bidi_rba;             // records of each ring in its producer's (unused) tree-level area;
-                            // the other bidi_rb - bidi_rba behind the chain areas
   // ---- two-ended trajectories in a migrating launch's tail (0: off) ----
   // once at most tail_left chains of the launch are unfinished, a chain alone in its tile
-  // recruits two of the tile's idle receivers as producers and books its trees itself;
-  // rings of bidi_rb = bidi_rba records in the producers' tree-level areas
+  // recruits two of the tile's idle receivers as producers (their own chain areas)
   int tail_bidi;
   int tail_left;
   unsigned long long* bidi_count;   // two-ended transitions of the launch (fitoct_result)
@@ -140,7 +135,7 @@ struct KParams {
   // waves (nuts_device.hip "paired tiles"); the grid is 16 * ceil(pair_tiles / 8) blocks
   int pair;
   int pair_tiles;           // tiles of the launch (the tile map's entries)
-  int pair_stride;          // doubles per pair in pair_buf: start (4 vectors + 8) | bidi_rb records
+  int pair_stride;          // doubles per pair in pair_buf: start (4 vectors + 8) | record (5 + 16)
   int pair_test_absent;     // test hook (FITOCT_TEST_PAIR_ABSENT): partners leave at once
   int* pair_hdr;            // [pair_tiles][PAIR_HDR_INTS] hand-off words, zeroed per launch
   double* pair_buf;         // [pair_tiles][pair_stride]

@@ -128,6 +128,14 @@ struct ChainScalars {
   double spec_h;
   // Hamiltonian -lp + K(p) of each pool candidate and of the sample (energy__)
   double pool_h[MAXDEPTH + 1], smp_h;
+  // the running subtree's sum of the leaves' acceptance terms (added to sum_metro when the
+  // subtree ends, so two-ended trajectories can sum per subtree and stay bitwise equal)
+  double sub_metro;
+  // two-ended trajectories, a producer's record of its last subtree (Chain::sub_publish):
+  // the sample's lp, sum r^2 and energy, the subtree's weight, acceptance sum; its weight's
+  // exponent, leaves, flags (SR_VALID / SR_DIVERGENT), depth; vectors: SR_* below
+  double r_slp, r_ss2, r_sh, r_twm, r_metro;
+  int r_twe, r_n, r_flags, r_depth;
   long long prof[2][32];   // diagnostic build: cycles and calls per action
 };
 static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
@@ -257,14 +265,14 @@ constexpr unsigned long long MIG_WAIT_TICKS = 120ULL * TICKS_PER_S;
 // (relaxed agent-scope atomics: global_load / global_store ... sc1, no L1 copy on either
 // side), so no L2 write-back or invalidation is needed whichever XCDs the two tiles sit on.
 // Per pair: PAIR_HDR_INTS hand-off words (zeroed before every launch), then in pair_buf
-// the transition's start and a ring of bidi_rb leaf records.
+// the transition's start and one subtree record of the forward end.
 // ---------------------------------------------------------------------------
 enum PairHdr : int {
   // primary -> partner: the transition (its start is in pair_buf; -1: the chain finished),
-  // the helper's booked leaves of the forward end and the booked depth, each (gen << 16) | v;
+  // the booking's records taken of the forward end and the booked depth, each (gen << 16) | v;
   // the chain's index and the transition's number t
   PH_GEN = 0, PH_CONS = 1, PH_DEPTH = 2, PH_LC = 3, PH_T = 4,
-  PH_COUNT = 32,   // partner -> primary: (gen << 16) | forward-end records in the ring
+  PH_COUNT = 32,   // partner -> primary: (gen << 16) | forward-end subtree records published
   PH_STATE = 48    // PairState bits (both, atomics); PAIR_HDR_INTS words per pair (kernel_params.h)
 };
 // The pair's hand-shake: the primary marks START when it begins; the partner joins (START ->
@@ -871,8 +879,12 @@ struct Lds {
   // tiles of one or two chains (deep speculation): per chain, the booked leaf's q,
   // end-updated p, g, lp and sum r^2, handed from the chain's wave to its helper wave
   static constexpr int HX_BYTES = ((3 * VLEN + 2) * 8 + 15) / 16 * 16;
+  // two-ended trajectories (G = 3 areas: the chain's, two producers'): per producer, the leaf
+  // it hands its booking helper (q, end-updated p, g, lp, sum r^2, depth, leaf, transition)
+  static constexpr int PX_BYTES = ((3 * VLEN + 8) * 8 + 15) / 16 * 16;
   static __host__ __device__ constexpr int bytes(int G, int max_depth) {
-    return head_bytes(G) + G * chain_bytes(max_depth) + (G <= 2 ? G * HX_BYTES : 0);
+    return head_bytes(G) + G * chain_bytes(max_depth) +
+           (G <= 2 ? G * HX_BYTES : G == 3 ? 2 * PX_BYTES : 0);
   }
   AS_LDS char* base;
   int G, cb;
@@ -888,10 +900,13 @@ struct Lds {
   __device__ AS_LDS double* sums(int c) const { return vecs(c) + NVEC * VLEN; }
   __device__ AS_LDS double* aux(int c) const { return sums(c) + NSLOT; }
   __device__ AS_LDS double* lvls(int c) const { return aux(c) + NAUX; }
-  // chain c's hand-off block (G <= 2); hx(0) is also where a two-ended tile's (G = 3
-  // areas) ring extension starts
+  // chain c's hand-off block (G <= 2)
   __device__ AS_LDS double* hx(int c = 0) const {
     return (AS_LDS double*)(base + head_bytes(G) + G * cb + c * HX_BYTES);
+  }
+  // producer s's hand-off block (two-ended trajectories, G = 3)
+  __device__ AS_LDS double* px(int s) const {
+    return (AS_LDS double*)(base + head_bytes(G) + G * cb + s * PX_BYTES);
   }
 };
 
@@ -1047,6 +1062,7 @@ struct Chain {
   double krow[KROW ? NNP : 1];
   const AS_LDS double* bv;
   int lane, slot, lc, gid, nct;
+  int pix;   // proposal pool region: the chain's (lc); a two-ended producer's own (produce)
   // speculative leaves (the SPEC sampler): always in a tile of one chain (with a helper
   // wave), else while the tile hosts <= P.spec_live live chains (the tail of a launch, when
   // the sweep no longer hides the sampler's latency; this wave then does the helper's part)
@@ -1090,10 +1106,11 @@ struct Chain {
         part(L.part()), Kinv(L.kinv()), bv(L.bv()),
         lane(lane_), slot(slot_), lc(lc_), nct(nct_) {
     gid = Pr().chain_offset + lc;
+    pix = lc;
     // tiles of G <= 2 chains: NUTS wave G + c helps chain slot c (tile of one chain: wave 1)
     helped = SPEC && !MIG && P_.G <= 2;
     deep = helped;
-    HX = L.hx(L.G <= 2 ? slot_ : 0);   // (two-ended: L.G = 3, one ring extension)
+    HX = L.hx(L.G <= 2 ? slot_ : 0);
     bidi = kTwoEnded && !MIG && deep && P_.bidi != 0;
     key = make_key(Pr().seed, (uint32_t)gid);
     if constexpr (KROW) {
@@ -1109,8 +1126,7 @@ struct Chain {
 
   __device__ __forceinline__ KPc& Pr() const { return *pp; }
   // two-ended trajectories: producer k's chain area (NUTS slot bd[TW_SLOT + k] of this
-  // tile: the chain areas are consecutive, chain_bytes apart), its scalars, vectors and
-  // tree-level area (where the first bidi_rba records of its ring sit)
+  // tile: the chain areas are consecutive, chain_bytes apart), its scalars and vectors
   __device__ __forceinline__ AS_LDS char* parea(int k) const {
     const int sl = __builtin_amdgcn_readfirstlane(bd[TW_SLOT + k]);
     return (AS_LDS char*)Sp + (sl - slot) * Lds<PPL>::chain_bytes(Pr().max_depth);
@@ -1120,9 +1136,6 @@ struct Chain {
   }
   __device__ __forceinline__ AS_LDS double* pvb(int k) const {
     return (AS_LDS double*)(parea(k) + sizeof(ChainScalars));
-  }
-  __device__ __forceinline__ AS_LDS double* plv(int k) const {
-    return pvb(k) + NVEC * VLEN + NSLOT + NAUX;
   }
   __device__ __forceinline__ int idx(int s) const { return s * WAVE + lane; }
   __device__ __forceinline__ bool ok(int s) const { return idx(s) < Pr().D; }
@@ -1158,7 +1171,7 @@ struct Chain {
   __device__ __forceinline__ AS_GLB double* pslot(int sl, int which) const {
     // HBM [chain][max_depth+1][NPOOL][VLEN]; recomputed from the parameter block
     // on use (scalar ops) instead of holding a 64-bit pointer across actions
-    const size_t base = ((size_t)lc * (Pr().max_depth + 1) + sl) * NPOOL + which;
+    const size_t base = ((size_t)pix * (Pr().max_depth + 1) + sl) * NPOOL + which;
     return (AS_GLB double*)Pr().stack + base * VLEN;
   }
 
@@ -1794,6 +1807,7 @@ struct Chain {
     Sp->cur_lp = Sp->end_lp[dir];
     Sp->cur_s2 = Sp->end_s2[dir];
     Sp->leaf = 0;
+    Sp->sub_metro = 0.0;
     if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;   // merge uniforms are per subtree (depth d)
     const double e = dir ? Sp->eps_used : -Sp->eps_used;
     Sp->lf_e = e;
@@ -1924,6 +1938,7 @@ struct Chain {
       Sp->cur_lp = Sp->end_lp[k_dirn];
       Sp->cur_s2 = Sp->end_s2[k_dirn];
       Sp->leaf = 0;
+      Sp->sub_metro = 0.0;
       if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;
       Sp->lf_e = k_dirn ? Sp->eps_used : -Sp->eps_used;
     }
@@ -1965,6 +1980,7 @@ struct Chain {
       Sp->dir = dirn;
       st(V_PNEAR, ld((dirn ? V_E1_Q : V_E0_Q) + 1));
       Sp->leaf = 0;
+      Sp->sub_metro = 0.0;
       if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;
       Sp->lf_e = dirn ? Sp->eps_used : -Sp->eps_used;
     }
@@ -1991,22 +2007,31 @@ struct Chain {
   }
 
   // ---------------- two-ended trajectories (P.bidi; tiles of one chain) ----------------
-  // Stan's trajectory grows by doublings in directions drawn per depth (TAG_DIR), and the
-  // leaves of all doublings in one direction form one unbroken leapfrog chain from the
-  // transition's start (a new subtree starts from the end the previous one in that direction
-  // left).  So the backward and the forward chain can be integrated at once, by two producer
-  // waves (slots 1 and 2) sharing the tile's gradient waves, while the helper books the leaves
-  // in tree order from their rings -- the same leaves, momenta, gradients and bookkeeping as the
-  // one-ended path, so the same draws; the period per transition falls from the sum of the two
-  // chains' leaves towards the longer one.  The chain's wave only starts and ends transitions.
-  // record n of stream s: [q (D) | end-updated p (D) | g (D) | lp | sum r^2] in the LDS ring
-  // behind the three chain areas (where HX would be)
-  // (the first bidi_rba records of ring s sit in producer slot s + 1's tree-level area, which
-  // a producer never uses)
-  __device__ AS_LDS double* brec(int s, int n) const {
-    const int rb = Pr().bidi_rb, ra = Pr().bidi_rba, m = n % rb;
-    return m < ra ? plv(s) + m * Pr().bidi_rec
-                  : HX + (s * (rb - ra) + (m - ra)) * Pr().bidi_rec;
+  // Stan's trajectory grows by doublings in directions drawn per depth (TAG_DIR); a doubling of
+  // depth d builds a subtree of 2^d leaves from the trajectory end in its direction, and the
+  // subtrees grown in one direction form one unbroken leapfrog chain from the transition's
+  // start.  Everything base_nuts::build_tree does inside a subtree -- each leaf's weight and
+  // divergence test, the multinomial merges, the U-turn checks of its levels, the subtree's
+  // proposal -- depends only on that subtree's leaves.  So two producer waves (one per
+  // direction, slots 1 and 2) build the subtrees of their direction whole, each in its own
+  // chain area (levels, merge uniforms, proposal pool), at most BIDI_LOOK doublings past the
+  // one booked, and the chain's wave books the trajectory level only, in tree order, from one
+  // record per subtree (sub_publish): the top-level multinomial merge, the new end, the
+  // trajectory-level U-turn checks.  The same operations on the same values as the one-ended
+  // path (the acceptance statistic is summed per subtree on every path), so the same draws;
+  // a transition takes about as long as its longer end, and the booking no longer paces it.
+  enum SubRes : int { SL_MID = 0, SL_DONE = 1, SL_END = 2 };
+  enum SubFlag : int { SR_VALID = 1, SR_DIVERGENT = 2 };
+  // a producer's subtree record, in vectors of its own chain area that a producer never uses:
+  // the proposal's q and g, the end's (last leaf's) momentum, the subtree's begin momentum and
+  // momentum sum; its scalars are ChainScalars::r_*
+  static constexpr int SR_SQ = V_SMP_Q, SR_SG = V_SMP_G, SR_EP = V_E1_P, SR_PB = V_E1_Q,
+                       SR_RHO = V_RHO, SR_NVEC = 5;
+  __device__ __forceinline__ V pld(const AS_LDS double* base, int v) const {
+    V r;
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) r.a[s] = base[v * VLEN + idx(s)];
+    return r;
   }
   // a migrating tile's chain, at the start of a transition (depth 0): two-ended when the tile
   // hosts one live chain, two idle receivers of the tile have become
@@ -2022,23 +2047,27 @@ struct Chain {
     if (lane == 0) ok = atomicCAS((int*)&bd[TW_BUSY], 0, 1) == 0;
     return uni(__shfl(ok, 0)) != 0;
   }
-  // Book every leaf of transition g in Stan's tree order from the producers' rings: the
-  // helper wave of a tile of one chain, or a migrating tile's chain itself.  LB_END, with
-  // the status ERR_TIMEOUT if a producer's record never came (a fault)
-  // profiling build: the booking wave's cycles waiting for records / booking, leaves booked
+  // The chain's wave: book transition g's trajectory level in Stan's tree order from the
+  // producers' subtree records (base_nuts::transition: the loop over depths; top_merge and
+  // leaf_book's trajectory check on the record's values).  LB_END, with the status
+  // ERR_TIMEOUT if a producer's record never came (a fault)
+  // profiling build: this wave's cycles waiting for records / booking, subtrees booked
   long long pf_wait = 0, pf_busy = 0, pf_n = 0;
-  __device__ int bidi_book_tree(const int g) {
-    int cons0 = 0, cons1 = 0;
+  __device__ __forceinline__ int bidi_book_tree(const int g) {
+    const uint32_t t = (uint32_t)uni(Sp->t);
+    const V minv = ld(V_MINV);
+    int m0 = 0, m1 = 0;
     for (;;) {
       const long long pt0 = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
-      const int s = uni(Sp->dir);   // the subtree being booked grows this end
-      const int n = s ? cons1 : cons0;
+      const int d = uni(Sp->depth);
+      const int s = (uniform(key, t, TAG_DIR, (uint32_t)d, 0u) > 0.5) ? 1 : 0;
+      const int m = s ? m1 : m0;
       bool lost = false;
-      Patience wl;   // one producer leaf: its throttle never holds back the leaf booked next
-      for (;;) {     // leaf n of stream s published for this transition
+      Patience wl;   // one subtree of the longer end: bounded by the whole tree's bound
+      for (;;) {     // record m of end s published for this transition
         const int w = bd[BD_PROD + s];
-        if ((w >> 16) == g && (w & 0xFFFF) > n) break;
-        if (bd[BD_GEN] != g || wl.expired(LEAF_WAIT_TICKS)) {   // never, short of a fault
+        if ((w >> 16) == g && (w & 0xFFFF) > m) break;
+        if (bd[BD_GEN] != g || wl.expired(MIG_WAIT_TICKS)) {   // never, short of a fault
           lost = true;
           break;
         }
@@ -2050,30 +2079,62 @@ struct Chain {
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the record after its count
       const long long pt1 = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
-      const int r = bidi_book(s, n);
-      if (s) ++cons1;
-      else ++cons0;
-      wave_publish();
-      if (lane == 0) bd[BD_CONS + s] = n + 1;
+      const AS_LDS ChainScalars* R = psp(s);
+      const AS_LDS double* RV = pvb(s);
+      const int fl = uni(R->r_flags);
+      Sp->n_leapfrog = uni(Sp->n_leapfrog) + uni(R->r_n);
+      Sp->sum_metro = Sp->sum_metro + R->r_metro;
+      if (fl & SR_DIVERGENT) Sp->divergent = 1;
+      bool persist = false;
+      if (fl & SR_VALID) {
+        // top_merge: the sample, the trajectory's weight, the end, the depth
+        const XF Tw{R->r_twm, uni(R->r_twe)};
+        const XF Ww{Sp->lsw_m, Sp->lsw_e};
+        const double u_top = uniform(key, t, TAG_TOP, (uint32_t)d, 0u);
+        const bool take = xf_gt(Tw, Ww) || xf_u_below(u_top, Tw, Ww);
+        if (take) {
+          st(V_SMP_Q, pld(RV, SR_SQ));
+          st(V_SMP_G, pld(RV, SR_SG));
+          Sp->smp_lp = R->r_slp;
+          Sp->smp_s2 = R->r_ss2;
+          Sp->smp_h = R->r_sh;
+        }
+        const XF Wn = xf_add(Ww, Tw);
+        Sp->lsw_m = Wn.m;
+        Sp->lsw_e = Wn.e;
+        Sp->depth = d + 1;
+        // the trajectory-level U-turn checks (leaf_book's, at the subtree's last leaf)
+        const V pend = pld(RV, SR_EP), Tpb = pld(RV, SR_PB), Trho = pld(RV, SR_RHO);
+        const int ef = s ? V_E1_P : V_E0_P;
+        const V far = ld(s ? V_E0_P : V_E1_P), near = ld(ef), rho = ld(V_RHO);
+        V rtot, rx, ry;
+#pragma unroll
+        for (int k = 0; k < PPL; ++k) {
+          rtot.a[k] = rho.a[k] + Trho.a[k];
+          rx.a[k] = rho.a[k] + Tpb.a[k];
+          ry.a[k] = Trho.a[k] + near.a[k];
+        }
+        persist = crit3(far, pend, rtot, far, Tpb, rx, near, pend, ry, minv);
+        st(ef, pend);
+        st(V_RHO, rtot);
+      }
+      if (s) ++m1;
+      else ++m0;
+      wave_publish();   // the record's reads are done before the slot is released
+      if (lane == 0) bd[BD_CONS + s] = m + 1;
       if (kProfile) {
         pf_wait += pt1 - pt0;
         pf_busy += (long long)__builtin_amdgcn_s_memtime() - pt1;
         ++pf_n;
       }
-      if (r == LB_END) return LB_END;
+      if (!persist || d + 1 >= Pr().max_depth) return LB_END;
     }
   }
-  // the chain's wave, at depth 0 of a transition: act_begin_subtree's bookkeeping, the start
-  // to both producers' slots, then the transition's number (BD_GEN) releases them
+  // the chain's wave, at depth 0 of a transition: the start to both producers' slots, then
+  // the transition's number (BD_GEN) releases them
   __device__ int bidi_begin() {
     const uint32_t t = (uint32_t)uni(Sp->t);
-    const int dir = (uniform(key, t, TAG_DIR, 0u, 0u) > 0.5) ? 1 : 0;
-    Sp->dir = dir;
     const V q = ld(V_E0_Q), p = ld(V_E0_P), g = ld(V_E0_G), minv = ld(V_MINV);   // E0 = E1 = start
-    st(V_PNEAR, p);
-    Sp->leaf = 0;
-    if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;
-    Sp->lf_e = dir ? Sp->eps_used : -Sp->eps_used;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       AS_LDS double* const pv = pvb(k);
@@ -2088,8 +2149,7 @@ struct Chain {
       if (lane == 0) {
         ps->eps_used = Sp->eps_used;
         ps->t = (int)t;
-        ps->end_lp[0] = Sp->end_lp[0];
-        ps->end_s2[0] = Sp->end_s2[0];
+        ps->H0 = Sp->H0;
       }
     }
     if (lane == 0) {
@@ -2105,20 +2165,134 @@ struct Chain {
     }
     return A_BIDI_TREE;
   }
-  // the helper: book leaf n of stream s (published: its record is in the ring).  Lanes past D
-  // read 0, the value every padding lane of q, p and g holds
-  __device__ int bidi_book(int s, int n) {
-    const AS_LDS double* r = brec(s, n);
-    const int D = Pr().D;
-    V q, pe, g;
-#pragma unroll
-    for (int k = 0; k < PPL; ++k) {
-      const bool in = ok(k);
-      q.a[k] = in ? r[idx(k)] : 0.0;
-      pe.a[k] = in ? r[D + idx(k)] : 0.0;
-      g.a[k] = in ? r[2 * D + idx(k)] : 0.0;
+  // ---- the producer's side (run on the producer's own chain area) ----
+  // a subtree of depth d begins (act_begin_subtree's bookkeeping, counts of this subtree)
+  __device__ void sub_begin(const int d) {
+    Sp->depth = d;
+    Sp->leaf = 0;
+    Sp->sub_metro = 0.0;
+    Sp->n_leapfrog = 0;
+    Sp->pool_used = 0;
+    Sp->divergent = 0;
+    if (lane < MAXDEPTH) Sp->u_blk[lane] = -1;
+  }
+  // One leaf of the producer's subtree (base_nuts::build_tree below the trajectory level):
+  // leaf_book's weight, divergence test, merges, U-turn checks and push -- the same operations
+  // on the same values.  At the subtree's last leaf (SL_DONE) its weight, proposal, begin
+  // momentum and momentum sum are returned for sub_publish.  (q, p, g): the leaf with its
+  // end-updated momentum.
+  __device__ __forceinline__ int sub_leaf(const V& q, const V& p, const V& g, const V& minv, const double cur_lp,
+                          const double cur_s2, XF& Tw_o, int& Tprop_o, V& Tpb_o, V& Trho_o,
+                          double& h_o) {
+    const double H0 = Sp->H0;
+    const double sub_metro0 = Sp->sub_metro;
+    const int d = uni(Sp->depth), j = uni(Sp->leaf), nlf = uni(Sp->n_leapfrog);
+    unsigned used = (unsigned)uni(Sp->pool_used);
+    Sp->n_leapfrog = nlf + 1;
+    tree_uniforms(d, j, (uint32_t)uni(Sp->t));   // this leaf's merge uniforms
+    double h = -cur_lp + kin(p, minv);
+    if (isnan(h)) h = INFINITY;
+    const double wl = H0 - h;
+    const XF wleaf = xf_exp<FV3>(wl);
+    Sp->sub_metro = sub_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
+    if (h - H0 > 1000.0) {   // divergent: the transition ends here
+      Sp->divergent = 1;
+      return SL_END;
     }
-    return book_leaf(q, pe, g, r[3 * D], r[3 * D + 1]);
+    V Tpb = p, Trho = p;
+    XF Tw = wleaf;
+    int Tprop = -1;   // -1: the current leaf; else a pool slot
+#pragma unroll 1
+    for (int l = 0; l < d; ++l) {
+      if (((j >> l) & 1) == 0) {   // push T as the init subtree of level l+1
+        lst(l, K_PBEG, Tpb);
+        lst(l, K_PEND, p);
+        lst(l, K_RHO, Trho);
+        Sp->st_w_m[l] = Tw.m;
+        Sp->st_w_e[l] = Tw.e;
+        Sp->st_prop[l] = (Tprop < 0) ? pool_put(used, q, g, cur_lp, cur_s2, h) : Tprop;
+        break;
+      }
+      // merge init I = level l with final T (base_nuts::build_tree at depth l+1)
+      const V Ipb = lld(l, K_PBEG), Ipe = lld(l, K_PEND), Irho = lld(l, K_RHO);
+      const XF Iw{Sp->st_w_m[l], Sp->st_w_e[l]};
+      const double um = RNG[l * WAVE + ((j >> (l + 1)) & (WAVE - 1))];
+      const int Iprop = uni(Sp->st_prop[l]);
+      const XF Sw = xf_add(Iw, Tw);
+      const bool take_final = xf_gt(Tw, Sw) || xf_u_below(um, Tw, Sw);
+      if (take_final) {
+        used &= ~(1u << Iprop);
+      } else {
+        if (Tprop >= 0) used &= ~(1u << Tprop);
+        Tprop = Iprop;
+      }
+      V rsub, rx, ry;
+#pragma unroll
+      for (int s = 0; s < PPL; ++s) {
+        rsub.a[s] = Irho.a[s] + Trho.a[s];
+        rx.a[s] = Irho.a[s] + Tpb.a[s];
+        ry.a[s] = Trho.a[s] + Ipe.a[s];
+      }
+      const bool okc = crit3(Ipb, p, rsub, Ipb, Tpb, rx, Ipe, p, ry, minv);
+      Tpb = Ipb;
+      Trho = rsub;
+      Tw = Sw;
+      if (!okc) {
+        Sp->pool_used = (int)used;
+        return SL_END;
+      }
+    }
+    Sp->pool_used = (int)used;
+    if (j != (1 << d) - 1) {
+      Sp->leaf = j + 1;
+      return SL_MID;
+    }
+    Tw_o = Tw;
+    Tprop_o = Tprop;
+    Tpb_o = Tpb;
+    Trho_o = Trho;
+    h_o = h;
+    return SL_DONE;
+  }
+  // the subtree's record for the booking (its slot free: the previous record was booked).
+  // flags 0 / SR_DIVERGENT: an invalid subtree (only its counts matter)
+  __device__ __forceinline__ void sub_publish(const int flags, const XF Tw, const int Tprop, const V& Tpb,
+                              const V& Trho, const V& q, const V& pe, const V& g, const double lp,
+                              const double s2, const double h) {
+    if (flags & SR_VALID) {
+      V sq = q, sg = g;
+      double slp = lp, ss2 = s2, sh = h;
+      if (Tprop >= 0) {   // the proposal is a pool slot (top_merge's read)
+        const AS_GLB double* pq = pslot(Tprop, P_Q);
+        const AS_GLB double* pg = pslot(Tprop, P_G);
+#pragma unroll
+        for (int s = 0; s < PPL; ++s) {
+          sq.a[s] = ok(s) ? pq[idx(s)] : 0.0;
+          sg.a[s] = ok(s) ? pg[idx(s)] : 0.0;
+        }
+        slp = Sp->pool_lp[Tprop];
+        ss2 = Sp->pool_s2[Tprop];
+        sh = Sp->pool_h[Tprop];
+      }
+      st(SR_SQ, sq);
+      st(SR_SG, sg);
+      st(SR_EP, pe);
+      st(SR_PB, Tpb);
+      st(SR_RHO, Trho);
+      if (lane == 0) {
+        Sp->r_slp = slp;
+        Sp->r_ss2 = ss2;
+        Sp->r_sh = sh;
+        Sp->r_twm = Tw.m;
+        Sp->r_twe = Tw.e;
+      }
+    }
+    if (lane == 0) {
+      Sp->r_metro = Sp->sub_metro;
+      Sp->r_n = Sp->n_leapfrog;
+      Sp->r_flags = flags;
+      Sp->r_depth = Sp->depth;
+    }
   }
 
   // run by the helper wave for the leaf being booked: its Hamiltonian and multinomial
@@ -2194,7 +2368,7 @@ struct Chain {
     FITOCT_MARK(act_leaf_split);
     long long ts = stamp0();
     const double H0 = Sp->H0;
-    const double sum_metro0 = Sp->sum_metro;
+    const double sub_metro0 = Sp->sub_metro;
     const int d = uni(Sp->depth), j = uni(Sp->leaf), nlf = uni(Sp->n_leapfrog);
     unsigned used = (unsigned)uni(Sp->pool_used);
     Sp->n_leapfrog = nlf + 1;
@@ -2239,10 +2413,12 @@ struct Chain {
     // phase B: the leaf's weight (book_leaf's, or this wave's own: act_spec_book)
     const double h = Sp->spec_h, wl = H0 - h;
     const XF wleaf{Sp->spec_wm, uni(Sp->spec_we)};
-    Sp->sum_metro = sum_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
+    const double sm = sub_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
+    Sp->sub_metro = sm;
     sub(1, ts);
     if (h - H0 > 1000.0) {   // divergent: the transition ends here
       Sp->divergent = 1;
+      Sp->sum_metro += sm;
       return LB_END;
     }
     XF Tw = wleaf;
@@ -2265,6 +2441,7 @@ struct Chain {
     }
     if (fail < nm) {
       Sp->pool_used = (int)used;
+      Sp->sum_metro += sm;
       return LB_END;
     }
     if (nm < d) {   // push the running subtree as the init subtree of level nm + 1
@@ -2283,6 +2460,7 @@ struct Chain {
     }
     // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
     top_merge(q, p, g, cur_lp, cur_s2, h, Tw, Tprop, used, dir, d);
+    Sp->sum_metro += sm;
     st(V_RHO, rtot);
     sub(3, ts);
     if (!persist || d + 1 >= Pr().max_depth) return LB_END;
@@ -2298,7 +2476,7 @@ struct Chain {
     FITOCT_MARK(act_leaf);
     long long ts = stamp0();
     const double H0 = Sp->H0;
-    const double sum_metro0 = Sp->sum_metro;
+    const double sub_metro0 = Sp->sub_metro;
     const int d = uni(Sp->depth), j = uni(Sp->leaf), nlf = uni(Sp->n_leapfrog);
     unsigned used = (unsigned)uni(Sp->pool_used);
     Sp->n_leapfrog = nlf + 1;
@@ -2307,10 +2485,15 @@ struct Chain {
     sub(0, ts);
     const double wl = H0 - h;
     const XF wleaf = xf_exp<FV3>(wl);
-    Sp->sum_metro = sum_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
+    // (Stan sums these over the trajectory's leaves in order; here per subtree, then the
+    // subtrees' sums in tree order: a reassociation of the same terms, so that two-ended
+    // trajectories, whose subtrees are booked by their producers, give the same bits)
+    const double sm = sub_metro0 + ((wl > 0.0) ? 1.0 : xf_val(wleaf));
+    Sp->sub_metro = sm;
     sub(1, ts);
     if (h - H0 > 1000.0) {   // divergent: the transition ends here
       Sp->divergent = 1;
+      Sp->sum_metro += sm;
       return LB_END;
     }
 
@@ -2354,6 +2537,7 @@ struct Chain {
       Tw = Sw;
       if (!okc) {
         Sp->pool_used = (int)used;
+        Sp->sum_metro += sm;
         return LB_END;
       }
     }
@@ -2366,6 +2550,7 @@ struct Chain {
     // the subtree of depth d is complete and valid: top-level merge (base_nuts::transition)
     const int dir = uni(Sp->dir);
     top_merge(q, p, g, cur_lp, cur_s2, h, Tw, Tprop, used, dir, d);
+    Sp->sum_metro += sm;
     const V far = ld(dir ? V_E0_P : V_E1_P), near = ld(V_PNEAR), rho = ld(V_RHO);
     V rtot, rx, ry;
 #pragma unroll
@@ -2797,7 +2982,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   // a request for the bookkeeping of its leaf (deep: the leaf in HX[c]) or the prior part of
   // a speculated position; its helper wave (NUTS wave G + c) runs it and publishes the
   // request number it finished
-  __shared__ int help_req[2], help_done[2], help_res[2];
+  __shared__ int help_req[2], help_done[2], help_res[2], help_seen[2], help_gen[2], help_m[2];
   const bool spec = SPEC;
   const bool helped = SPEC && !MIG && P.G <= 2;   // spare NUTS waves help the tile's chains
   const bool bidi = Chain<PPL, NNP, FAM, MIG, SPEC>::kTwoEnded && helped &&
@@ -2846,9 +3031,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     }
   }
   if (tid < 2) {
-    help_req[tid] = 0;
+    // (a partner tile has no backward-end producer: its helper serves producer 1 only)
+    help_req[tid] = (role == 1 && tid == 0) ? -1 : 0;
     help_done[tid] = 0;
     help_res[tid] = 0;
+    help_seen[tid] = 0;
+    help_gen[tid] = 0;
+    help_m[tid] = 0;
   }
   if (tid < GMAX) {
     grad_cnt[tid] = 0;
@@ -2965,16 +3154,21 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     const bool mig = MIG && P.mig != nullptr;
     using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
     // Two-ended trajectories: producer of trajectory end s (0: backward, 1: forward) on NUTS
-    // slot `slot` (its chain area holds the end's state; its ring of leaf records sits in the
-    // area's tree levels and, in a tile of one chain, behind the chain areas).  For every
-    // transition g the chain starts (BD_GEN), it leapfrogs this end from the start through
-    // the doublings drawn in direction s, at most BIDI_LOOK doublings past the one
-    // being booked and a ring ahead of the booking, and publishes each leaf's record.
-    // `epoch`: the slot's sweeps so far (grad_cnt[slot] counts NGW per sweep).  Ends with
-    // BD_GEN < 0 (the tile's chain finished) or, in a migrating tile, with the launch.
+    // slot `slot` (its chain area holds the end's state, its subtree's levels and merge
+    // uniforms, and its last subtree's record; its proposal pool is its own).  For every
+    // transition g the chain starts (BD_GEN), it builds the subtrees of the doublings drawn in
+    // direction s from the start outwards (Chain::sub_leaf), at most BIDI_LOOK doublings past
+    // the one booked, and publishes one record per subtree once the booking has taken the
+    // previous one.  `epoch`: the slot's sweeps so far (grad_cnt[slot] counts NGW per sweep).
+    // Ends with BD_GEN < 0 (the tile's chain finished) or, in a migrating tile, with the launch.
+    // helped: a helper wave books this end's leaves (nuts_device.hip serve; tiles of one chain),
+    // else the producer books them itself (a migrating launch's tail)
+    constexpr bool helped = !MIG;
     auto produce = [&](const int s, const int slot, long long epoch) {
+      int hreq = 0;   // leaves handed to the helper
       Ch pr(P, L, slot, c0, lane, nct);
       pr.bd = (volatile AS_LDS int*)bd;
+      pr.pix = P.chains + (c0 / P.G) * GMAX + slot;   // its own proposal pool region
       int seen = 0;
       bool quit = false;
       // profiling build: cycles waiting for sweeps, for the lookahead / ring room, leaves,
@@ -3010,32 +3204,25 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         const Vd<PPL> minv = pr.ld(V_MINV);
         const double eps = pr.Sp->eps_used;
         const uint32_t t = (uint32_t)pr.uni(pr.Sp->t);
-        // lane k: this end's leaves through doubling k (directions: act_begin_subtree's draws)
-        int cum = 0;
-        if (lane < P.max_depth) {
-          const int dk = (uniform(pr.key, t, TAG_DIR, (uint32_t)lane, 0u) > 0.5) ? 1 : 0;
-          cum = (dk == s) ? (1 << lane) : 0;
-        }
-#pragma unroll
-        for (int o = 1; o < MAXDEPTH; o <<= 1) {
-          const int v = __shfl_up(cum, o);
-          if (lane >= o) cum += v;
-        }
+        // bit k: doubling k grows in direction s (act_begin_subtree's draws)
+        const bool mine = lane < P.max_depth &&
+                          ((uniform(pr.key, t, TAG_DIR, (uint32_t)lane, 0u) > 0.5) ? 1 : 0) == s;
+        const unsigned long long dmask = __builtin_amdgcn_ballot_w64(mine);
         wave_fence();
         if (lds_load(&bd[BD_GEN]) != g) continue;   // the start was rewritten while read
         const double e = s ? eps : -eps;
-        // may leaf n of this end grow now: within BIDI_LOOK doublings of the booked one,
-        // and the ring.  Once true it stays true for the transition (the booked depth and the
-        // helper's count only grow), so a check made while a sweep runs holds after it
-        auto may = [&](const int n) -> bool {
-          const int dl = min(pr.uni(*(volatile const AS_LDS int*)&S0.depth) + BIDI_LOOK,
-                             P.max_depth - 1);
-          const int lim = pr.uni(__shfl(cum, dl));
-          const int cons = lds_load(&bd[BD_CONS + s]);
-          return n < lim && n - cons < P.bidi_rb;
+        // this end's next doubling after depth d (-1: none)
+        auto next_depth = [&](const int d) -> int {
+          const unsigned long long r = d < 0 ? dmask : dmask & ~((2ULL << d) - 1);
+          return r ? (int)__builtin_ctzll(r) : -1;
+        };
+        // may the subtree of depth d grow now: within BIDI_LOOK doublings of the booked depth.
+        // Once true it stays true for the transition (the booked depth only grows)
+        auto may = [&](const int d) -> bool {
+          return d <= pr.uni(*(volatile const AS_LDS int*)&S0.depth) + BIDI_LOOK;
         };
         const long long pft0 = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
-        auto wait_may = [&](const int n) -> bool {   // false: the tree ended
+        auto wait_may = [&](const int d) -> bool {   // false: the tree ended
           Patience w;
           const long long pt = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
           for (;;) {
@@ -3043,13 +3230,27 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
               if (kProfile) pf_may += (long long)__builtin_amdgcn_s_memtime() - pt;
               return false;
             }
-            if (may(n)) {
+            if (may(d)) {
               if (kProfile) pf_may += (long long)__builtin_amdgcn_s_memtime() - pt;
               return true;
             }
             // the other end may grow for long (deep trees, large N).  In effect this wait
             // ends with BD_GEN: its bound outlasts the bound on the whole tree (MIG_WAIT_TICKS
             // from the tree's start), after which BD_GEN changes
+            if (w.expired(2 * MIG_WAIT_TICKS)) return false;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        };
+        // the record slot is free once the booking has taken records 0 .. m - 1
+        auto wait_room = [&](const int m) -> bool {   // false: the tree ended
+          Patience w;
+          const long long pt = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
+          for (;;) {
+            if (lds_load(&bd[BD_GEN]) != g) return false;
+            if (lds_load(&bd[BD_CONS + s]) >= m) {
+              if (kProfile) pf_may += (long long)__builtin_amdgcn_s_memtime() - pt;
+              return true;
+            }
             if (w.expired(2 * MIG_WAIT_TICKS)) return false;
             __builtin_amdgcn_s_sleep(1);
           }
@@ -3071,16 +3272,18 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           }
           ++epoch;
         };
-        if (!wait_may(0)) continue;
+        int d = next_depth(-1);
+        if (d < 0 || !wait_may(d)) continue;
+        if (!helped) pr.sub_begin(d);   // (helped: the helper begins a subtree at its leaf 0)
+        int m = 0;   // subtree records published this transition (not helped)
+        int j = 0;   // the leaf in its sweep: leaf j of the subtree of depth d
         stage(q, p, gr);
         pr.prior_part();
-        // leaf n is in its sweep here.  Its successor is staged before leaf n's record is
-        // written whenever the successor may grow already (checked while the sweep runs):
-        // the record write and the checks leave the end's critical path
-        for (int n = 0;; ++n) {
-          // (a migrating launch's tail keeps the record-first order: config 3 measured -1.3 %
-          // with the successor staged first, config 2 +13.7 %; profiles/r05_ab_stage.txt)
-          const bool pre = !MIG && may(n + 1);
+        // a leaf is in its sweep here.  Once it is in, the next one (in this subtree, or the
+        // first of this end's next subtree if that may grow already) is staged first and the
+        // leaf's bookkeeping runs during that sweep: the next position depends only on this
+        // leaf's q, p and g (if the bookkeeping ends the subtree, that sweep is dropped)
+        for (;;) {
           bool late = false;
           Patience ws;
           const long long pt = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -3101,8 +3304,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           }
           wave_fence();
           // read with the partial sums (its latency hides in finish_grad's): a leaf the tree
-          // no longer needs is dropped; one published just after the tree ends is ignored
-          // (the count carries its transition)
+          // no longer needs is dropped
           const int gen_now = lds_load(&bd[BD_GEN]);
           Vd<PPL> gn;
           double s2;
@@ -3112,31 +3314,87 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           for (int k = 0; k < PPL; ++k) pe.a[k] = fma(0.5 * e, gn.a[k], p1.a[k]);   // end_update_p
           if (gen_now != g) break;   // the tree has ended: the leaf is not needed
           const Vd<PPL> qn = q1;
-          if (pre) stage(qn, pe, gn);
-          AS_LDS double* r = pr.brec(s, n);
-          const int D = P.D;
-#pragma unroll
-          for (int k = 0; k < PPL; ++k) {
-            if (pr.ok(k)) {
-              r[pr.idx(k)] = qn.a[k];
-              r[D + pr.idx(k)] = pe.a[k];
-              r[2 * D + pr.idx(k)] = gn.a[k];
+          const bool last = j == (1 << d) - 1;
+          const int dn = last ? next_depth(d) : d;
+          const bool nxt = !last || (dn >= 0 && may(dn));
+          if (nxt) stage(qn, pe, gn);
+          if (helped) {
+            // hand this leaf to the booking helper once it has booked the previous one; stop
+            // when that booking cut its subtree (nothing later on this end is needed)
+            if (hreq > 0) {
+              Patience wh;
+              bool gone = false;
+              while (lds_load(&help_done[s]) < hreq) {
+                if (lds_load(&bd[BD_GEN]) != g || wh.expired(LEAF_WAIT_TICKS)) {
+                  gone = true;
+                  break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+              }
+              if (gone) break;
+              const int res = lds_load(&help_res[s]);
+              if ((res >> 2) == g && (res & 3) == Ch::SL_END) break;
             }
+            AS_LDS double* X = L.px(s);
+#pragma unroll
+            for (int k = 0; k < PPL; ++k) {
+              X[pr.idx(k)] = qn.a[k];
+              X[Ch::VLEN + pr.idx(k)] = pe.a[k];
+              X[2 * Ch::VLEN + pr.idx(k)] = gn.a[k];
+            }
+            if (lane == 0) {
+              X[3 * Ch::VLEN] = lp;
+              X[3 * Ch::VLEN + 1] = s2;
+              X[3 * Ch::VLEN + 2] = (double)d;
+              X[3 * Ch::VLEN + 3] = (double)j;
+              X[3 * Ch::VLEN + 4] = (double)g;
+            }
+            wave_publish();   // the leaf lands before its request number
+            ++hreq;
+            if (lane == 0) __atomic_store_n(&help_req[s], hreq, __ATOMIC_RELAXED);
+            if (last) {
+              if (dn < 0) break;   // this end has no further doubling in this tree
+              if (!nxt) {
+                if (!wait_may(dn)) break;
+                stage(qn, pe, gn);
+              }
+              d = dn;
+              j = 0;
+            } else {
+              ++j;
+            }
+            pr.prior_part();
+            continue;
           }
-          if (lane == 0) {
-            r[3 * D] = lp;
-            r[3 * D + 1] = s2;
-          }
-          wave_publish();   // the record lands before its count
-          if (lane == 0) __atomic_store_n(&bd[BD_PROD + s], (g << 16) | (n + 1), __ATOMIC_RELAXED);
-          if (!pre) {
-            if (!wait_may(n + 1)) break;
-            stage(qn, pe, gn);
+          XF Tw{0.0, 0};
+          int Tprop = -1;
+          Vd<PPL> Tpb = pe, Trho = pe;
+          double h = 0.0;
+          const int r = pr.sub_leaf(qn, pe, gn, minv, lp, s2, Tw, Tprop, Tpb, Trho, h);
+          if (r != Ch::SL_MID) {   // the subtree is complete (or cut): its record for the booking
+            if (!wait_room(m)) break;
+            const int fl = r == Ch::SL_DONE ? Ch::SR_VALID
+                                            : pr.uni(pr.Sp->divergent) ? Ch::SR_DIVERGENT : 0;
+            pr.sub_publish(fl, Tw, Tprop, Tpb, Trho, qn, pe, gn, lp, s2, h);
+            wave_publish();   // the record lands before its count
+            ++m;
+            if (lane == 0) __atomic_store_n(&bd[BD_PROD + s], (g << 16) | m, __ATOMIC_RELAXED);
+            if (r == Ch::SL_END || dn < 0) break;   // this end adds nothing more to the tree
+            if (!nxt) {
+              if (!wait_may(dn)) break;
+              stage(qn, pe, gn);
+            }
+            d = dn;
+            j = 0;
+            pr.sub_begin(d);
+          } else {
+            ++j;
           }
           pr.prior_part();
         }
         if (kProfile) pf_tree += (long long)__builtin_amdgcn_s_memtime() - pft0;
       }
+      if (helped && lane == 0) __atomic_store_n(&help_req[s], -1, __ATOMIC_RELAXED);   // its helper may leave
       if (kProfile && P.stamps != nullptr && lane == 0) {   // this end's producer (either tile)
         AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)tix * NSTAMP + 88 + 4 * s;
         o[0] = pf_sw;
@@ -3145,28 +3403,100 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         o[3] = pf_tree;
       }
     };
+    // Two-ended trajectories in a tile of one chain: the booking helper (NUTS wave 1 of the tile,
+    // and of a partner tile) books the leaves its producers hand over -- Chain::sub_leaf on the
+    // producer's own chain area, its subtree record once the subtree ends (when the booking has
+    // taken the previous one) -- while the producer completes the next gradient and stages the
+    // one after.  One request of producer s: 1 served, 0 none pending, -1 the producer is gone.
+    // (help_seen / help_gen / help_m: requests served, and the transition and records published
+    // of producer s, kept by the helper.)
+    auto serve = [&](const int s) -> int {
+      const int rq = lds_load(&help_req[s]);
+      if (rq < 0) return -1;
+      if (rq == lds_load(&help_seen[s])) return 0;
+      wave_fence();   // the leaf after its request number
+      Ch hc(P, L, 1 + s, c0, lane, nct);
+      hc.bd = (volatile AS_LDS int*)bd;
+      hc.pix = P.chains + (c0 / P.G) * GMAX + 1 + s;
+      const AS_LDS double* X = L.px(s);
+      Vd<PPL> q, pe, gg;
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) {
+        q.a[k] = X[hc.idx(k)];
+        pe.a[k] = X[Ch::VLEN + hc.idx(k)];
+        gg.a[k] = X[2 * Ch::VLEN + hc.idx(k)];
+      }
+      const double lp = X[3 * Ch::VLEN], s2 = X[3 * Ch::VLEN + 1];
+      const int d = __builtin_amdgcn_readfirstlane((int)X[3 * Ch::VLEN + 2]);
+      const int j = __builtin_amdgcn_readfirstlane((int)X[3 * Ch::VLEN + 3]);
+      const int gen = __builtin_amdgcn_readfirstlane((int)X[3 * Ch::VLEN + 4]);
+      int r = Ch::SL_END;
+      if (lds_load(&bd[BD_GEN]) == gen) {   // (else a leaf of a tree that has ended)
+        hc.key = make_key(P.seed, (uint32_t)(P.chain_offset + lds_load(&bd[TW_LC])));
+        int hm = lds_load(&help_m[s]);
+        if (lds_load(&help_gen[s]) != gen) hm = 0;
+        if (j == 0) hc.sub_begin(d);
+        XF Tw{0.0, 0};
+        int Tprop = -1;
+        Vd<PPL> Tpb = pe, Trho = pe;
+        double h = 0.0;
+        r = hc.sub_leaf(q, pe, gg, hc.ld(V_MINV), lp, s2, Tw, Tprop, Tpb, Trho, h);
+        if (r != Ch::SL_MID) {   // the subtree ended: its record, once the slot is free
+          Patience w;
+          bool room = true;
+          while (lds_load(&bd[BD_CONS + s]) < hm) {
+            if (lds_load(&bd[BD_GEN]) != gen || w.expired(2 * MIG_WAIT_TICKS)) {
+              room = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (room) {
+            const int fl = r == Ch::SL_DONE ? Ch::SR_VALID
+                                            : hc.uni(hc.Sp->divergent) ? Ch::SR_DIVERGENT : 0;
+            hc.sub_publish(fl, Tw, Tprop, Tpb, Trho, q, pe, gg, lp, s2, h);
+            wave_publish();   // the record lands before its count
+            ++hm;
+            if (lane == 0) __atomic_store_n(&bd[BD_PROD + s], (gen << 16) | hm, __ATOMIC_RELAXED);
+          } else {
+            r = Ch::SL_END;
+          }
+        }
+        if (lane == 0) {
+          help_m[s] = hm;
+          help_gen[s] = gen;
+        }
+      }
+      wave_publish();   // the booking's LDS writes land before its result
+      if (lane == 0) {
+        help_seen[s] = rq;
+        __atomic_store_n(&help_res[s], (gen << 2) | r, __ATOMIC_RELAXED);
+        wave_publish();
+        __atomic_store_n(&help_done[s], rq, __ATOMIC_RELAXED);
+      }
+      return 1;
+    };
     // ---- paired tiles (P.pair): the bridge waves.  The forward end's producer runs unchanged
-    // in the partner tile (NUTS wave 3, chain area 2, its own ring in LDS); two bridge waves make
-    // the pair look like one tile to it and to the primary's helper:
+    // in the partner tile (NUTS wave 3, chain area 2); two bridge waves make the pair look like
+    // one tile to it and to the primary's booking:
     //   bridge_in (primary, NUTS wave 3, where that producer would run): each transition's start
-    //     (producer area 2, written by bidi_begin) and the helper's progress on the forward end
-    //     (booked leaves, booked depth) out to the pair's words; the partner's leaf records in
-    //     from the pair's ring into the primary's forward ring, published as a local producer
-    //     would (BD_PROD + 1);
+    //     (producer area 2, written by bidi_begin) and the end of each tree, and the booking's
+    //     progress (records of the forward end taken, booked depth) out to the pair's words;
+    //     the partner's subtree records in, into the primary's area 2, published as a local
+    //     producer would (BD_PROD + 1);
     //   bridge_out (partner, NUTS wave 2): the start into the producer's area and BD_GEN; the
-    //     helper's progress into BD_CONS + 1 and the depth the producer's lookahead reads; the
-    //     producer's records out to the pair's ring, then PH_COUNT.
-    // Every record reaches the helper only through both bridges, and the producer may overwrite
-    // ring slot n % rb only once the helper has booked leaf n (its ring-room check reads the
-    // mirrored, never larger, booked count), so one flow count guards all three rings.  Counts
-    // and the booked depth carry their transition (gen << 16) and only grow within it.
-    // the forward end's producer area (NUTS slot 2) and its ring (Chain::brec(1, n))
-    auto fwd_rec = [&](const int n) -> AS_LDS double* {
-      const int rb = P.bidi_rb, ra = P.bidi_rba, m = n % rb;
-      return m < ra ? L.lvls(2) + m * P.bidi_rec : L.hx(0) + ((rb - ra) + (m - ra)) * P.bidi_rec;
+    //     booking's progress into BD_CONS + 1 and the depth the producer's lookahead reads;
+    //     the producer's records out to the pair's record slot, then PH_COUNT.
+    // A record reaches the booking only through both bridges, and the producer writes record
+    // m only once the (mirrored, never larger) count of records booked is m, so one count
+    // guards the record's three slots.  Counts and the booked depth carry their transition
+    // (gen << 16) and only grow within it.
+    constexpr int RV = Ch::SR_NVEC;   // record vectors; then 16 scalars
+    auto rvec = [](const int v) {      // the record's v-th vector in a chain area
+      return v == 0 ? Ch::SR_SQ : v == 1 ? Ch::SR_SG : v == 2 ? Ch::SR_EP : v == 3 ? Ch::SR_PB : Ch::SR_RHO;
     };
     auto pair_start = [&]() { return xb; };
-    auto pair_ring = [&]() { return xb + 4 * Ch::VLEN + PAIR_START_DOUBLES; };
+    auto pair_rec = [&]() { return xb + 4 * Ch::VLEN + PAIR_START_DOUBLES; };
     auto bridge_in = [&]() -> bool {   // false: the pair did not form (grow the end here)
       {
         Patience w;   // the chain's first transition (or its end)
@@ -3184,9 +3514,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       st = __builtin_amdgcn_readfirstlane(__shfl(st, 0));
       if ((st & PS_LOCAL) || !(st & PS_JOIN)) return false;
       constexpr int VL = Ch::VLEN;
-      const int nrec = 3 * P.D + 2, rb = P.bidi_rb, rec = P.bidi_rec;
       AS_GLB double* const xs = pair_start();
-      AS_GLB double* const xr0 = pair_ring();
+      AS_GLB double* const xr = pair_rec();
+      AS_LDS double* const av = L.vecs(2);        // producer area 2: the start, the record
+      AS_LDS ChainScalars* const as = &L.cs(2);
       const volatile AS_LDS int* depth = (const volatile AS_LDS int*)&L.cs(0).depth;
       int seen = 0, copied = 0, last_cons = -1, last_depth = -1;
       Patience idle;
@@ -3197,28 +3528,27 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             if (lane == 0) x_sti(xh + PH_GEN, -1);
             break;
           }
-          wave_fence();   // the start after its number
-          const AS_LDS double* pv = L.vecs(2);
-          const AS_LDS ChainScalars* ps = &L.cs(2);
+          if (!(g & BD_ENDED)) {   // a new transition: its start first
+            wave_fence();   // the start after its number
 #pragma unroll
-          for (int s = 0; s < PPL; ++s) {
-            const int k = s * WAVE + lane;
-            x_st(xs + k, pv[V_E0_Q * VL + k]);
-            x_st(xs + VL + k, pv[V_E0_P * VL + k]);
-            x_st(xs + 2 * VL + k, pv[V_E0_G * VL + k]);
-            x_st(xs + 3 * VL + k, pv[V_MINV * VL + k]);
+            for (int s = 0; s < PPL; ++s) {
+              const int k = s * WAVE + lane;
+              x_st(xs + k, av[V_E0_Q * VL + k]);
+              x_st(xs + VL + k, av[V_E0_P * VL + k]);
+              x_st(xs + 2 * VL + k, av[V_E0_G * VL + k]);
+              x_st(xs + 3 * VL + k, av[V_MINV * VL + k]);
+            }
+            if (lane == 0) {
+              x_st(xs + 4 * VL, as->eps_used);
+              x_st(xs + 4 * VL + 1, as->H0);
+              x_sti(xh + PH_T, as->t);
+              x_sti(xh + PH_LC, lds_load(&bd[TW_LC]));
+            }
+            x_drain();   // the start has reached memory before its number
           }
           if (lane == 0) {
-            x_st(xs + 4 * VL, ps->eps_used);
-            x_st(xs + 4 * VL + 1, ps->end_lp[0]);
-            x_st(xs + 4 * VL + 2, ps->end_s2[0]);
-            x_sti(xh + PH_T, ps->t);
-            x_sti(xh + PH_LC, lds_load(&bd[TW_LC]));
-          }
-          x_drain();   // the start has reached memory before its number
-          if (lane == 0) {
-            x_sti(xh + PH_GEN, g);
-            atomicAdd(P.pair_count, 1ULL);
+            x_sti(xh + PH_GEN, g);   // (a tree's end: its number with BD_ENDED)
+            if (!(g & BD_ENDED)) atomicAdd(P.pair_count, 1ULL);
           }
           seen = g;
           copied = 0;
@@ -3226,7 +3556,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           idle = Patience{};
           continue;
         }
-        // the helper's progress on the forward end, for the partner's lookahead and ring room
+        // the booking's progress on the forward end, for the partner's lookahead and record slot
         const int cons = lds_load(&bd[BD_CONS + 1]);
         const int dep = *depth;
         if (lds_load(&bd[BD_GEN]) == seen) {
@@ -3235,31 +3565,46 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           last_cons = cons;
           last_depth = dep;
         }
-        // the partner's records of this transition
+        // the partner's next record of this transition
         const int pc = __builtin_amdgcn_readfirstlane(x_ldi(xh + PH_COUNT));
         if ((pc >> 16) == seen && (pc & 0xFFFF) > copied) {
-          const int cnt = pc & 0xFFFF;
-          for (int n = copied; n < cnt; ++n) {
-            const AS_GLB double* src = xr0 + (size_t)(n % rb) * rec;
-            AS_LDS double* dst = fwd_rec(n);
-            for (int i = lane; i < nrec; i += WAVE) dst[i] = x_ld(src + i);
+#pragma unroll
+          for (int v = 0; v < RV; ++v)
+#pragma unroll
+            for (int s = 0; s < PPL; ++s) {
+              const int k = s * WAVE + lane;
+              av[rvec(v) * VL + k] = x_ld(xr + v * VL + k);
+            }
+          if (lane == 0) {
+            const AS_GLB double* sc = xr + RV * VL;
+            as->r_slp = x_ld(sc);
+            as->r_ss2 = x_ld(sc + 1);
+            as->r_sh = x_ld(sc + 2);
+            as->r_twm = x_ld(sc + 3);
+            as->r_metro = x_ld(sc + 4);
+            as->r_twe = (int)x_ld(sc + 5);
+            as->r_n = (int)x_ld(sc + 6);
+            as->r_flags = (int)x_ld(sc + 7);
+            as->r_depth = (int)x_ld(sc + 8);
           }
-          wave_publish();   // the records land before their count
-          if (lane == 0) __atomic_store_n(&bd[BD_PROD + 1], (seen << 16) | cnt, __ATOMIC_RELAXED);
-          copied = cnt;
+          wave_publish();   // the record lands before its count
+          copied = pc & 0xFFFF;
+          if (lane == 0) __atomic_store_n(&bd[BD_PROD + 1], (seen << 16) | copied, __ATOMIC_RELAXED);
           idle = Patience{};
           continue;
         }
         if (idle.expired(2 * MIG_WAIT_TICKS)) break;   // never, short of a fault
         __builtin_amdgcn_s_sleep(1);
       }
+      if (lane == 0) __atomic_store_n(&help_req[1], -1, __ATOMIC_RELAXED);   // no producer 1 here
       return true;
     };
     auto bridge_out = [&]() {
       constexpr int VL = Ch::VLEN;
-      const int nrec = 3 * P.D + 2, rb = P.bidi_rb, rec = P.bidi_rec;
       AS_GLB double* const xs = pair_start();
-      AS_GLB double* const xr0 = pair_ring();
+      AS_GLB double* const xr = pair_rec();
+      AS_LDS double* const av = L.vecs(2);        // the producer's area
+      AS_LDS ChainScalars* const as = &L.cs(2);
       volatile AS_LDS int* depth = (volatile AS_LDS int*)&L.cs(0).depth;   // the producer's S0
       if (lane == 0) {
         bd[TW_CHAIN] = 0;
@@ -3273,24 +3618,23 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         const int dw = __builtin_amdgcn_readfirstlane(x_ldi(xh + PH_DEPTH));
         if (g != seen) {
           if (g < 0) break;
-          AS_LDS double* pv = L.vecs(2);
-          AS_LDS ChainScalars* ps = &L.cs(2);
+          if (!(g & BD_ENDED)) {   // a new transition: the start into the producer's area
 #pragma unroll
-          for (int s = 0; s < PPL; ++s) {
-            const int k = s * WAVE + lane;
-            pv[V_E0_Q * VL + k] = x_ld(xs + k);
-            pv[V_E0_P * VL + k] = x_ld(xs + VL + k);
-            pv[V_E0_G * VL + k] = x_ld(xs + 2 * VL + k);
-            pv[V_MINV * VL + k] = x_ld(xs + 3 * VL + k);
-          }
-          if (lane == 0) {
-            ps->eps_used = x_ld(xs + 4 * VL);
-            ps->end_lp[0] = x_ld(xs + 4 * VL + 1);
-            ps->end_s2[0] = x_ld(xs + 4 * VL + 2);
-            ps->t = x_ldi(xh + PH_T);
-            bd[TW_LC] = x_ldi(xh + PH_LC);
-            bd[BD_CONS + 1] = 0;
-            *depth = 0;
+            for (int s = 0; s < PPL; ++s) {
+              const int k = s * WAVE + lane;
+              av[V_E0_Q * VL + k] = x_ld(xs + k);
+              av[V_E0_P * VL + k] = x_ld(xs + VL + k);
+              av[V_E0_G * VL + k] = x_ld(xs + 2 * VL + k);
+              av[V_MINV * VL + k] = x_ld(xs + 3 * VL + k);
+            }
+            if (lane == 0) {
+              as->eps_used = x_ld(xs + 4 * VL);
+              as->H0 = x_ld(xs + 4 * VL + 1);
+              as->t = x_ldi(xh + PH_T);
+              bd[TW_LC] = x_ldi(xh + PH_LC);
+              bd[BD_CONS + 1] = 0;
+              *depth = 0;
+            }
           }
           wave_publish();   // the start lands before the transition's number
           if (lane == 0) __atomic_store_n(&bd[BD_GEN], g, __ATOMIC_RELAXED);
@@ -3299,22 +3643,35 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           idle = Patience{};
           continue;
         }
-        if (lane == 0) {   // the helper's progress: never lowered within the transition
+        if (lane == 0) {   // the booking's progress: never lowered within the transition
           if ((cw >> 16) == seen && (cw & 0xFFFF) > bd[BD_CONS + 1]) bd[BD_CONS + 1] = cw & 0xFFFF;
           if ((dw >> 16) == seen && (dw & 0xFFFF) > *depth) *depth = dw & 0xFFFF;
         }
         const int pw = lds_load(&bd[BD_PROD + 1]);
         if ((pw >> 16) == seen && (pw & 0xFFFF) > copied) {
-          const int cnt = pw & 0xFFFF;
-          wave_fence();   // the records after their count
-          for (int n = copied; n < cnt; ++n) {
-            const AS_LDS double* src = fwd_rec(n);
-            AS_GLB double* dst = xr0 + (size_t)(n % rb) * rec;
-            for (int i = lane; i < nrec; i += WAVE) x_st(dst + i, src[i]);
+          wave_fence();   // the record after its count
+#pragma unroll
+          for (int v = 0; v < RV; ++v)
+#pragma unroll
+            for (int s = 0; s < PPL; ++s) {
+              const int k = s * WAVE + lane;
+              x_st(xr + v * VL + k, av[rvec(v) * VL + k]);
+            }
+          if (lane == 0) {
+            AS_GLB double* sc = xr + RV * VL;
+            x_st(sc, as->r_slp);
+            x_st(sc + 1, as->r_ss2);
+            x_st(sc + 2, as->r_sh);
+            x_st(sc + 3, as->r_twm);
+            x_st(sc + 4, as->r_metro);
+            x_st(sc + 5, (double)as->r_twe);
+            x_st(sc + 6, (double)as->r_n);
+            x_st(sc + 7, (double)as->r_flags);
+            x_st(sc + 8, (double)as->r_depth);
           }
-          x_drain();   // every record has reached memory before the count
-          if (lane == 0) x_sti(xh + PH_COUNT, (seen << 16) | cnt);
-          copied = cnt;
+          x_drain();   // the record has reached memory before its count
+          copied = pw & 0xFFFF;
+          if (lane == 0) x_sti(xh + PH_COUNT, (seen << 16) | copied);
           idle = Patience{};
           continue;
         }
@@ -3332,38 +3689,20 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     };
     if constexpr (SPEC && !MIG) {
       if (role == 1 && pair_on && c == 2) bridge_out();   // partner tile: the bridge
-    }
-    if (bidi && role == 0 && c == 1) {   // two-ended trajectories: book every leaf in tree order
-      Ch ch(P, L, 0, c0, lane, nct);
-      ch.bd = (volatile AS_LDS int*)bd;
-      int seen = 0;
-      long long pf_idle = 0;
-      for (;;) {
-        int g;
-        Patience w;   // (init and step-size searches run between transitions)
-        bool quit = false;
-        const long long pt0 = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
-        while ((g = lds_load(&bd[BD_GEN])) == seen) {   // the next transition, or the end
-          if (w.expired(MIG_WAIT_TICKS)) {
-            quit = true;
-            break;
+      if (bidi && c == 1 && (role == 0 || pair_on)) {   // the booking helper of the producers
+        Patience w;
+        for (int s = 0;; s ^= 1) {   // (one call site: serve is inlined once)
+          const int a = serve(s);
+          if (a > 0) {
+            w = Patience{};
+            continue;
           }
-          __builtin_amdgcn_s_sleep(1);
+          if (a < 0 && lds_load(&help_req[s ^ 1]) < 0) break;   // both producers gone
+          if (s == 1) {
+            if (w.expired(MIG_WAIT_TICKS)) break;   // never, short of a fault
+            __builtin_amdgcn_s_sleep(1);
+          }
         }
-        if (kProfile) pf_idle += (long long)__builtin_amdgcn_s_memtime() - pt0;
-        if (quit || g < 0) break;
-        seen = g;
-        wave_fence();   // the transition's start state is read after its number
-        ch.bidi_book_tree(g);
-        wave_publish();   // the booking's LDS writes land before the end is published
-        if (lane == 0) __atomic_store_n(&bd[BD_END], g, __ATOMIC_RELAXED);
-      }
-      if (kProfile && P.stamps != nullptr && lane == 0) {   // the booking wave's time
-        AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)tix * NSTAMP;
-        o[84] = ch.pf_busy;
-        o[85] = ch.pf_wait;
-        o[86] = ch.pf_n;
-        o[87] = pf_idle;
       }
     }
     // two-ended trajectories: producer of the backward (c = 2) / forward end (c = 3); paired
@@ -3426,27 +3765,14 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           FITOCT_MARK(nuts_loop);
         const long long s0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
         const int y = ch.run(a);
-        if (Ch::kTwoEnded && y == Ch::A_BIDI_TREE) {   // the producers and the helper grow the tree
+        if (Ch::kTwoEnded && y == Ch::A_BIDI_TREE) {   // the producers grow the subtrees
           const int g = lds_load(&bd[BD_GEN]);
-          bool late = false;
-          if constexpr (MIG) {   // no helper wave in a migrating tile: the chain books itself
-            ch.bidi_book_tree(g);
-          } else {
-            Patience w;
-            while (lds_load(&bd[BD_END]) != g) {   // a whole tree
-              if (w.expired(MIG_WAIT_TICKS)) {
-                late = true;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
-            }
-          }
-          if constexpr (MIG) {   // the producers stop growing this tree
-            wave_publish();
-            if (lane == 0) {
-              __atomic_store_n(&bd[BD_GEN], g | BD_ENDED, __ATOMIC_RELAXED);
-              __atomic_store_n(&bd[TW_BUSY], 0, __ATOMIC_RELAXED);   // another chain may claim them
-            }
+          const bool late = false;
+          ch.bidi_book_tree(g);   // this wave books the trajectory level
+          wave_publish();   // the producers stop growing this tree
+          if (lane == 0) {
+            __atomic_store_n(&bd[BD_GEN], g | BD_ENDED, __ATOMIC_RELAXED);
+            __atomic_store_n(&bd[TW_BUSY], 0, __ATOMIC_RELAXED);   // (migrating tiles) another chain may claim them
           }
           wave_fence();   // the helper's bookkeeping is read after the end
           // the helper's booked leaves count toward the step bound like the chain's own
@@ -3579,7 +3905,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             atomicAdd(&chains_done_here, 1);
           }
           if (helped && lane == 0) __atomic_store_n(&help_req[c], -1, __ATOMIC_RELAXED);   // release the helper
-          if (bidi) {   // release the producers and the helper; the producers drain their sweeps
+          if (bidi) {   // release the producers; they drain their sweeps
+            if (kProfile && P.stamps != nullptr && lane == 0) {   // the booking's time
+              AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)tix * NSTAMP;
+              o[84] = ch.pf_busy;
+              o[85] = ch.pf_wait;
+              o[86] = ch.pf_n;
+            }
             if (lane == 0) __atomic_store_n(&bd[BD_GEN], -1, __ATOMIC_RELAXED);
             Patience w;
             while (lds_load(&bd[BD_EXIT]) < 2 && !w.expired(LEAF_WAIT_TICKS)) __builtin_amdgcn_s_sleep(1);
@@ -3736,11 +4068,6 @@ __global__ void __launch_bounds__(TPB, 2) logp_kernel(const KParams* __restrict_
 #define FITOCT_CAT(a, b) FITOCT_CAT2(a, b)
 
 #if FITOCT_FAMILY == 0
-// doubles of a chain area's tree levels and merge-uniform rings (two-ended trajectories keep
-// leaf records there in the producers' areas)
-int lvl_doubles(int ppl, int max_depth) {
-  return max_depth * NLVL * WAVE * ppl + max_depth * WAVE;
-}
 int lds_bytes(int ppl, int G, int max_depth) {
   return ppl == 1 ? Lds<1>::bytes(G, max_depth) : Lds<2>::bytes(G, max_depth);
 }
@@ -3754,10 +4081,8 @@ template <class R, int BPT, int NNP, int PPL, int MODE>
 static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int tiles,
                            hipStream_t st, const int* tile_map) {
   constexpr int F = FITOCT_FAMILY;
-  // two-ended trajectories: 3 chain areas, then the two leaf rings
-  const int lds = (!logp && P.bidi) ? Lds<PPL>::bytes(3, P.max_depth) +
-                                          2 * (P.bidi_rb - P.bidi_rba) * P.bidi_rec * 8
-                                    : Lds<PPL>::bytes(P.G, P.max_depth);
+  // two-ended trajectories: 3 chain areas (the chain's and its two producers')
+  const int lds = (!logp && P.bidi) ? Lds<PPL>::bytes(3, P.max_depth) : Lds<PPL>::bytes(P.G, P.max_depth);
   if (logp) {
     auto k = logp_kernel<R, BPT, NNP, PPL, MODE, F>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

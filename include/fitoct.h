@@ -169,9 +169,9 @@ typedef struct fitoct_plan_info {
    * forward ends on two spare waves at once; same draws bit for bit).  two_ended = 1 when
    * the plan's one-chain tiles run them, 2 (ABI 7) when a migrating plan's chains do so once
    * alone in their tile (the launch's tail: two idle receivers of the tile become the
-   * producers), 0 when off; ring_records = leaf records per end's LDS ring,
-   * ring_records_in_levels = how many of them sit in the producer's tree-level area (the
-   * rest extend the LDS carve); both 0 when off. */
+   * producers), 0 when off.  ABI 7: each end's producer builds its subtrees whole and hands
+   * the booking one record per subtree: ring_records = 1 (records in flight per end) when on,
+   * ring_records_in_levels = 0 (kept for layout); both 0 when off. */
   int32_t two_ended;
   int32_t ring_records;
   int32_t ring_records_in_levels;

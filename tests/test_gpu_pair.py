@@ -2,13 +2,13 @@
 tiles fit on the chip twice (2 x tiles <= CUs: config 2's 128 chains on 256 CUs, config 5's
 8-GPU share, the reference's own 4-chain call, server.R:469), each tile's trajectory grows
 its forward end in a partner workgroup with its own four gradient waves; bridge waves in
-the two tiles carry the transition's start, the booking's progress and the leaf records
+the two tiles carry the transition's start, the booking's progress and the subtree records
 through write-through (sc1) global memory.
 
 The partner runs the same producer on the same values, so draws, step sizes, metrics, last
 positions and leapfrog counts must equal the unpaired two-ended path (FITOCT_NO_PAIR=1) and
-the one-ended path (FITOCT_NO_BIDI=1) bit for bit -- for every prior family, tiny rings
-(the flow count guards the three rings of a record's path), tile counts that are not a
+the one-ended path (FITOCT_NO_BIDI=1) bit for bit -- for every prior family, deep trees
+(one count guards the three slots of a subtree record's path), tile counts that are not a
 multiple of 8 (padding blocks), batches, and when partners never join
 (FITOCT_TEST_PAIR_ABSENT=1: every primary grows both ends itself after the hand-shake)."""
 from __future__ import annotations
@@ -23,8 +23,7 @@ from test_gpu_sampler import _prob
 
 pytestmark = pytest.mark.gpu
 
-ENV = ("FITOCT_NO_PAIR", "FITOCT_NO_BIDI", "FITOCT_BIDI_RB", "FITOCT_TEST_PAIR_ABSENT",
-       "FITOCT_NO_SPEC")
+ENV = ("FITOCT_NO_PAIR", "FITOCT_NO_BIDI", "FITOCT_TEST_PAIR_ABSENT", "FITOCT_NO_SPEC")
 
 
 def _with_env(env, fn):
@@ -57,18 +56,18 @@ def _same(a, b):
     assert a.total_leapfrogs == b.total_leapfrogs
 
 
-@pytest.mark.parametrize("family,N,chains,depth,rb", [
-    ("normal", 512, 128, 10, None),     # config 2's shape: 128 tiles -> 256 workgroups
-    ("lasso", 300, 24, 8, None),        # 24 tiles: the last group of 8 is whole
-    ("horseshoe", 2048, 37, 8, None),   # 37 tiles: padding blocks in the last group of 16
-    ("normal", 481, 4, 10, None),       # the reference's 4-chain call (server.R:469)
-    ("horseshoe", 512, 16, 7, "3"),     # rings of 3 records: producer throttled by the booking
+@pytest.mark.parametrize("family,N,chains,depth", [
+    ("normal", 512, 128, 10),     # config 2's shape: 128 tiles -> 256 workgroups
+    ("lasso", 300, 24, 8),        # 24 tiles: the last group of 8 is whole
+    ("horseshoe", 2048, 37, 8),   # 37 tiles: padding blocks in the last group of 16
+    ("normal", 481, 4, 10),       # the reference's 4-chain call (server.R:469)
+    ("horseshoe", 512, 16, 12),   # deep trees: the record slot throttles the producers
 ])
-def test_paired_tiles_preserve_draws_bitwise(family, N, chains, depth, rb):
+def test_paired_tiles_preserve_draws_bitwise(family, N, chains, depth):
     prob = _prob(family, N, 15)
     cfg = SamplerConfig(chains=chains, warmup=80, samples=60, seed=41, max_treedepth=depth)
-    info, a = _plan_run(prob, cfg, FITOCT_BIDI_RB=rb)
-    i1, b = _plan_run(prob, cfg, FITOCT_BIDI_RB=rb, FITOCT_NO_PAIR="1")
+    info, a = _plan_run(prob, cfg)
+    i1, b = _plan_run(prob, cfg, FITOCT_NO_PAIR="1")
     i2, c = _plan_run(prob, cfg, FITOCT_NO_BIDI="1")
     assert info["chains_per_tile"] == 1 and info["two_ended"] == 1 and info["paired"] == 1
     assert info["workgroups"] == 16 * ((info["tiles"] + 7) // 8)

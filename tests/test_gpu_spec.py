@@ -143,43 +143,35 @@ def test_headline_tiles_fit_four_chains_at_depth_12():
             assert pl.info["sampler"] == 3 and pl.info["lds_bytes"] <= 160 * 1024
 
 
-@pytest.mark.parametrize("family,N,Nn,depth,rb", [
-    ("normal", 512, 15, 10, None), ("normal", 512, 15, 4, "2"), ("horseshoe", 2048, 15, 8, "3"),
-    ("lasso", 300, 15, 12, None),
-    # rings past the tree-level area: deep horseshoe trees put > ring_records_in_levels
-    # leaves on one end, so records land in the LDS extension behind the chain areas
-    ("horseshoe", 2048, 15, 10, None),
+@pytest.mark.parametrize("family,N,Nn,depth", [
+    ("normal", 512, 15, 10), ("normal", 512, 15, 4), ("horseshoe", 2048, 15, 8),
+    ("lasso", 300, 15, 12), ("horseshoe", 2048, 15, 10),
     # Nn = 20: two parameters per lane (the ppl = 2 chain areas), shallow enough to fit
-    ("normal", 512, 20, 6, None)])
-def test_two_ended_trajectories_preserve_draws_bitwise(family, N, Nn, depth, rb):
-    """Tiles of one chain grow both ends of each trajectory at once (two producer waves,
-    leaf rings in the tile's LDS -- first the producers' own tree-level areas, then an
-    extension behind the three chain areas --, the helper booking in tree order;
-    nuts_device.hip "Two-ended trajectories"): same draws, step sizes, metrics and
-    leapfrog counts as the one-ended deep-speculation path (FITOCT_NO_BIDI=1), also with
-    rings of 2-3 records (producers throttled by the booking), trees cut at max_treedepth
-    4, and the ppl = 2 carve (Nn = 20).  The plan reports the mode and its rings (ABI 6)."""
+    ("normal", 512, 20, 6)])
+def test_two_ended_trajectories_preserve_draws_bitwise(family, N, Nn, depth):
+    """Tiles of one chain grow both ends of each trajectory at once: two producer waves build
+    the subtrees of each direction whole (weights, merges, U-turn checks, proposal) in chain
+    areas of their own and hand the chain's wave one record per subtree, which it books at the
+    trajectory level in Stan's tree order (nuts_device.hip "two-ended trajectories").  Same
+    draws, step sizes, metrics and leapfrog counts as the one-ended deep-speculation path
+    (FITOCT_NO_BIDI=1), with trees cut at max_treedepth 4 and the ppl = 2 carve (Nn = 20).
+    The plan reports the mode and its records in flight per end (ABI 7: one).  With up to
+    128 such tiles on the chip the tiles are also paired (test_gpu_pair.py); here both."""
     prob = _prob(family, N, Nn)
     cfg = SamplerConfig(chains=24, warmup=80, samples=60, seed=35, max_treedepth=depth)
-    info, a = _run_env(prob, cfg, FITOCT_NO_BIDI=None, FITOCT_BIDI_RB=rb, FITOCT_NO_SPEC=None)
-    info0, b = _run_env(prob, cfg, FITOCT_NO_BIDI="1", FITOCT_BIDI_RB=None, FITOCT_NO_SPEC=None)
-    assert info["chains_per_tile"] == 1 and info["sampler"] == 2
-    assert info["two_ended"] == 1 and info0["two_ended"] == 0 and info0["ring_records"] == 0
-    rba, rbn = info["ring_records_in_levels"], info["ring_records"]
-    assert 1 <= rba <= rbn <= 256
-    if rb is not None:
-        assert rbn == int(rb)
-    else:
-        assert rbn >= 4 and info["lds_bytes"] <= 160 * 1024 - 1024
-        assert info["lds_bytes"] > info0["lds_bytes"]   # the producers' two chain areas (+ rings)
-    if (family, depth, rb) == ("horseshoe", 10, None):
-        # some transition has >= 2 (rba + 1) leapfrogs, so one end produced > rba leaves
-        # into ring slots [rba, rb): the extension was written and read
-        assert rbn > rba + 1 and a.draws[:, :, 4].max() >= 2 * (rba + 1), (rba, rbn)
-    np.testing.assert_array_equal(a.draws, b.draws)
-    np.testing.assert_array_equal(a.stepsize, b.stepsize)
-    np.testing.assert_array_equal(a.inv_metric, b.inv_metric)
-    assert a.total_leapfrogs == b.total_leapfrogs
+    for pair in (None, "1"):
+        info, a = _run_env(prob, cfg, FITOCT_NO_BIDI=None, FITOCT_NO_PAIR=pair, FITOCT_NO_SPEC=None)
+        info0, b = _run_env(prob, cfg, FITOCT_NO_BIDI="1", FITOCT_NO_PAIR=None, FITOCT_NO_SPEC=None)
+        assert info["chains_per_tile"] == 1 and info["sampler"] == 2
+        assert info["two_ended"] == 1 and info0["two_ended"] == 0 and info0["ring_records"] == 0
+        assert info["ring_records"] == 1 and info["ring_records_in_levels"] == 0
+        assert info["lds_bytes"] <= 160 * 1024 - 1024
+        assert info["lds_bytes"] > info0["lds_bytes"]   # the producers' two chain areas
+        assert a.two_ended_transitions > 0
+        np.testing.assert_array_equal(a.draws, b.draws)
+        np.testing.assert_array_equal(a.stepsize, b.stepsize)
+        np.testing.assert_array_equal(a.inv_metric, b.inv_metric)
+        assert a.total_leapfrogs == b.total_leapfrogs
 
 
 def test_two_ended_off_where_three_chain_areas_do_not_fit():
@@ -189,10 +181,10 @@ def test_two_ended_off_where_three_chain_areas_do_not_fit():
     usual 4 chains run and match the plain sampler bit for bit."""
     prob = _prob("normal", 512, 20)
     cfg = SamplerConfig(chains=4, warmup=60, samples=40, seed=21, max_treedepth=10)
-    info, a = _run_env(prob, cfg, FITOCT_NO_BIDI=None, FITOCT_BIDI_RB=None, FITOCT_NO_SPEC=None)
+    info, a = _run_env(prob, cfg, FITOCT_NO_BIDI=None, FITOCT_NO_SPEC=None)
     assert info["chains_per_tile"] == 1 and info["two_ended"] == 0
     assert info["lds_bytes"] <= 160 * 1024
-    _, b = _run_env(prob, cfg, FITOCT_NO_BIDI=None, FITOCT_BIDI_RB=None, FITOCT_NO_SPEC="1")
+    _, b = _run_env(prob, cfg, FITOCT_NO_BIDI=None, FITOCT_NO_SPEC="1")
     np.testing.assert_array_equal(a.draws, b.draws)
     assert np.all(np.isfinite(a.draws[:, :, 0]))
 
