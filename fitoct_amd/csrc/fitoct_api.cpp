@@ -848,6 +848,8 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
     k.tail_bidi = 1;
     k.tail_left = k.chains;   // from the start (config 3: +1.0 % over one per tile, profiles/r05_ab_tail_left.txt)
     if (const char* e = getenv("FITOCT_TAIL_LEFT")) k.tail_left = std::max(0, atoi(e));
+    if (const char* e = getenv("FITOCT_TEST_TAIL_IDLE_US"))   // test hook: producers give up early
+      k.tail_idle_ticks = 100ULL * (unsigned long long)std::max(1, atoi(e));
   }
   // (a batch pairs its tiles itself: fitoct_batch_create)
   if (g_chains == 0 && want_pairs(k, pl->tiles, pl->ncu)) {

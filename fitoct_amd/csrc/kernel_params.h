@@ -129,6 +129,9 @@ struct KParams {
   // recruits two of the tile's idle receivers as producers (their own chain areas)
   int tail_bidi;
   int tail_left;
+  // a tail producer idle this long (s_memrealtime ticks, 100 MHz) withdraws its role; 0:
+  // MIG_WAIT_TICKS (test hook FITOCT_TEST_TAIL_IDLE_US)
+  unsigned long long tail_idle_ticks;
   unsigned long long* bidi_count;   // two-ended transitions of the launch (fitoct_result)
   // ---- paired tiles (one-chain tiles with two-ended trajectories, 2 x tiles <= CUs; 0: off) ----
   // the forward end of each tile's trajectories grows in a partner tile with its own gradient

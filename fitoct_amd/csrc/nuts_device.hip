@@ -879,12 +879,13 @@ struct Lds {
   // tiles of one or two chains (deep speculation): per chain, the booked leaf's q,
   // end-updated p, g, lp and sum r^2, handed from the chain's wave to its helper wave
   static constexpr int HX_BYTES = ((3 * VLEN + 2) * 8 + 15) / 16 * 16;
-  // two-ended trajectories (G = 3 areas: the chain's, two producers'): per producer, the leaf
-  // it hands its booking helper (q, end-updated p, g, lp, sum r^2, depth, leaf, transition)
+  // two-ended trajectories (G = 3 areas: the chain's, two producers'): per producer, two
+  // slots for the leaves it hands its booking helper (q, end-updated p, g, lp, sum r^2, depth,
+  // leaf, transition)
   static constexpr int PX_BYTES = ((3 * VLEN + 8) * 8 + 15) / 16 * 16;
   static __host__ __device__ constexpr int bytes(int G, int max_depth) {
     return head_bytes(G) + G * chain_bytes(max_depth) +
-           (G <= 2 ? G * HX_BYTES : G == 3 ? 2 * PX_BYTES : 0);
+           (G <= 2 ? G * HX_BYTES : G == 3 ? 4 * PX_BYTES : 0);
   }
   AS_LDS char* base;
   int G, cb;
@@ -904,9 +905,9 @@ struct Lds {
   __device__ AS_LDS double* hx(int c = 0) const {
     return (AS_LDS double*)(base + head_bytes(G) + G * cb + c * HX_BYTES);
   }
-  // producer s's hand-off block (two-ended trajectories, G = 3)
-  __device__ AS_LDS double* px(int s) const {
-    return (AS_LDS double*)(base + head_bytes(G) + G * cb + s * PX_BYTES);
+  // producer s's hand-off slot k (two-ended trajectories, G = 3)
+  __device__ AS_LDS double* px(int s, int k) const {
+    return (AS_LDS double*)(base + head_bytes(G) + G * cb + (2 * s + k) * PX_BYTES);
   }
 };
 
@@ -2982,7 +2983,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   // a request for the bookkeeping of its leaf (deep: the leaf in HX[c]) or the prior part of
   // a speculated position; its helper wave (NUTS wave G + c) runs it and publishes the
   // request number it finished
-  __shared__ int help_req[2], help_done[2], help_res[2], help_seen[2], help_gen[2], help_m[2];
+  __shared__ int help_req[2], help_done[2], help_res[2], help_seen[2], help_gen[2], help_m[2],
+      help_dead[2];
   const bool spec = SPEC;
   const bool helped = SPEC && !MIG && P.G <= 2;   // spare NUTS waves help the tile's chains
   const bool bidi = Chain<PPL, NNP, FAM, MIG, SPEC>::kTwoEnded && helped &&
@@ -3038,6 +3040,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     help_seen[tid] = 0;
     help_gen[tid] = 0;
     help_m[tid] = 0;
+    help_dead[tid] = 0;
   }
   if (tid < GMAX) {
     grad_cnt[tid] = 0;
@@ -3179,8 +3182,28 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         {
           Patience w;
           int polls = 0;
+          const unsigned long long t_idle = MIG ? __builtin_amdgcn_s_memrealtime() : 0;
+          const unsigned long long idle_max = P.tail_idle_ticks ? P.tail_idle_ticks : MIG_WAIT_TICKS;
           while ((g = lds_load(&bd[BD_GEN])) == seen || (g > 0 && (g & BD_ENDED))) {
-            if (w.expired(MIG_WAIT_TICKS)) {
+            if (MIG) {
+              // a tail producer idle this long leaves -- but only once it holds TW_BUSY, so no
+              // chain claims the pair while it withdraws its role (TW_JOIN, its TW_CLAIM bit):
+              // a chain never waits for records of a producer that has gone.  While
+              // a chain holds TW_BUSY its tree is under way and the producer stays.
+              if (__builtin_amdgcn_s_memrealtime() - t_idle > idle_max) {
+                int gone = 0;
+                if (lane == 0 && atomicCAS((int*)&bd[TW_BUSY], 0, 2) == 0) {
+                  atomicSub((int*)&bd[TW_JOIN], 1);
+                  atomicAnd((int*)&bd[TW_CLAIM], ~(1 << s));
+                  __atomic_store_n(&bd[TW_BUSY], 0, __ATOMIC_RELAXED);
+                  gone = 1;
+                }
+                if (__builtin_amdgcn_readfirstlane(__shfl(gone, 0))) {
+                  quit = true;
+                  break;
+                }
+              }
+            } else if (w.expired(MIG_WAIT_TICKS)) {
               quit = true;
               break;
             }
@@ -3319,12 +3342,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           const bool nxt = !last || (dn >= 0 && may(dn));
           if (nxt) stage(qn, pe, gn);
           if (helped) {
-            // hand this leaf to the booking helper once it has booked the previous one; stop
-            // when that booking cut its subtree (nothing later on this end is needed)
+            // hand this leaf to the booking helper (two slots: once it has booked the leaf
+            // before the previous one); stop when a booking cut its subtree (nothing later on
+            // this end is needed)
             if (hreq > 0) {
               Patience wh;
               bool gone = false;
-              while (lds_load(&help_done[s]) < hreq) {
+              while (lds_load(&help_done[s]) < hreq - 1) {
                 if (lds_load(&bd[BD_GEN]) != g || wh.expired(LEAF_WAIT_TICKS)) {
                   gone = true;
                   break;
@@ -3335,7 +3359,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
               const int res = lds_load(&help_res[s]);
               if ((res >> 2) == g && (res & 3) == Ch::SL_END) break;
             }
-            AS_LDS double* X = L.px(s);
+            AS_LDS double* X = L.px(s, (hreq + 1) & 1);
 #pragma unroll
             for (int k = 0; k < PPL; ++k) {
               X[pr.idx(k)] = qn.a[k];
@@ -3411,14 +3435,15 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     // (help_seen / help_gen / help_m: requests served, and the transition and records published
     // of producer s, kept by the helper.)
     auto serve = [&](const int s) -> int {
-      const int rq = lds_load(&help_req[s]);
-      if (rq < 0) return -1;
-      if (rq == lds_load(&help_seen[s])) return 0;
+      const int rq0 = lds_load(&help_req[s]);
+      if (rq0 < 0) return -1;
+      const int rq = lds_load(&help_seen[s]) + 1;   // requests are served in order
+      if (rq > rq0) return 0;
       wave_fence();   // the leaf after its request number
       Ch hc(P, L, 1 + s, c0, lane, nct);
       hc.bd = (volatile AS_LDS int*)bd;
       hc.pix = P.chains + (c0 / P.G) * GMAX + 1 + s;
-      const AS_LDS double* X = L.px(s);
+      const AS_LDS double* X = L.px(s, rq & 1);
       Vd<PPL> q, pe, gg;
 #pragma unroll
       for (int k = 0; k < PPL; ++k) {
@@ -3431,7 +3456,9 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       const int j = __builtin_amdgcn_readfirstlane((int)X[3 * Ch::VLEN + 3]);
       const int gen = __builtin_amdgcn_readfirstlane((int)X[3 * Ch::VLEN + 4]);
       int r = Ch::SL_END;
-      if (lds_load(&bd[BD_GEN]) == gen) {   // (else a leaf of a tree that has ended)
+      // (else a leaf of a tree that has ended, or of a subtree a booking has cut: help_dead)
+      if (lds_load(&bd[BD_GEN]) == gen &&
+          !(lds_load(&help_gen[s]) == gen && lds_load(&help_dead[s]) == gen)) {
         hc.key = make_key(P.seed, (uint32_t)(P.chain_offset + lds_load(&bd[TW_LC])));
         int hm = lds_load(&help_m[s]);
         if (lds_load(&help_gen[s]) != gen) hm = 0;
@@ -3465,6 +3492,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if (lane == 0) {
           help_m[s] = hm;
           help_gen[s] = gen;
+          if (r == Ch::SL_END) help_dead[s] = gen;
         }
       }
       wave_publish();   // the booking's LDS writes land before its result

@@ -93,3 +93,22 @@ def test_tail_two_ended_preserves_draws_bitwise(family, N, left):
         np.testing.assert_array_equal(a.inv_metric, x.inv_metric)
         np.testing.assert_array_equal(a.last_q, x.last_q)
         assert a.total_leapfrogs == x.total_leapfrogs
+
+
+def test_tail_producer_that_gives_up_leaves_no_lone_chain_waiting():
+    """a tail producer idle past its bound (FITOCT_TEST_TAIL_IDLE_US=20: 20 us
+    instead of minutes) leaves its role only while it holds the tile's TW_BUSY word, and
+    withdraws it (TW_JOIN, its TW_CLAIM bit), so a lone chain never claims a pair with a
+    producer missing and then waits for records that no wave will write (ERR_TIMEOUT on a
+    healthy chain).  Producers come and go all through the tail here: every chain finishes,
+    with the draws of the launch without two-ended tails."""
+    prob = _prob("horseshoe", 512, 15)
+    cfg = SamplerConfig(chains=1024, warmup=100, samples=100, seed=29, max_treedepth=8)
+    info, a = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI=None, FITOCT_NO_MIGRATE=None,
+                       FITOCT_TEST_TAIL_IDLE_US="20")
+    _, b = _run_env(prob, cfg, FITOCT_NO_TAIL_BIDI="1", FITOCT_NO_MIGRATE=None,
+                    FITOCT_TEST_TAIL_IDLE_US=None)
+    assert info["two_ended"] == 2
+    np.testing.assert_array_equal(a.draws, b.draws)
+    np.testing.assert_array_equal(a.stepsize, b.stepsize)
+    assert a.total_leapfrogs == b.total_leapfrogs
