@@ -287,8 +287,10 @@ def test_headline_shape_hard_geometry_rhat_below_1_01(seed):
     chain traps, not whether the statements hold):
     - at most 0.3 % of the chains (3 of 1024) are trapped by the fixed rule
       (fitoct_amd.stanfit.trapped_chains: > 50 % divergent over the run or either half);
-    - a trapped chain stays trapped: its second-half divergence rate is > 50 % (the
-      funnel's neck at a fixed adapted step size is absorbing);
+    - (rounds 4-5 also asserted that a trapped chain stays trapped; round 6's per-subtree
+      acceptance sums moved the last bits, and at seed 1000 a chain 84 % divergent in the
+      first half of its draws escaped the funnel's neck in the second (0.2 %): the neck is
+      not absorbing, so that is no property of the sampler);
     - split and rank-normalised R-hat < 1.01 over the other chains, every parameter column
       but the inverse-gamma auxiliaries r2_*;
     - at the bench's seed, R-hat < 1.01 over ALL chains (the bench line's claim), and
@@ -300,15 +302,13 @@ def test_headline_shape_hard_geometry_rhat_below_1_01(seed):
     g = sample(prob, cfg)
     post = g.draws[:, cfg.warmup:, :]
     div = post[:, :, 5]
-    h = div.shape[1] // 2
     trapped = trapped_chains(div)
     assert trapped.sum() <= 3, np.where(trapped)[0]
-    assert np.all(div[trapped, h:].mean(1) > 0.5), div[trapped].mean(1)
     assert div[~trapped].mean() < 0.03
     cols = prob.column_names()
     par = [j for j, n in enumerate(cols) if j >= 7 and not n.startswith("r2_")]
     for keep in ([post[~trapped]] + ([post] if seed == 1000 else [])):
         rh = {cols[j]: split_rhat_ess(keep[:, :, j])[0] for j in par}
-        assert max(rh.values()) < 1.01, sorted(rh.items(), key=lambda t: -t[1])[:5]
         rr = {cols[j]: rank_rhat(keep[:, :, j]) for j in par}
+        assert max(rh.values()) < 1.01, sorted(rh.items(), key=lambda t: -t[1])[:5]
         assert max(rr.values()) < 1.01, sorted(rr.items(), key=lambda t: -t[1])[:5]
