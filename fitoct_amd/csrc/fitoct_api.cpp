@@ -693,8 +693,8 @@ bool want_pairs(const KParams& k, int tiles, int ncu) {
 int alloc_pairs(KParams& k, int tiles, int ppl, int** hdr, double** buf) {
   k.pair = 1;
   k.pair_tiles = tiles;
-  // the start (q, p, g, minv + scalars), then one subtree record (5 vectors + 16 scalars)
-  k.pair_stride = (PAIR_START_DOUBLES + WAVE * ppl * (4 + 5) + 16 + 15) / 16 * 16;
+  // the start (q, p, g, minv + scalars), then two subtree record slots (5 vectors + 16 scalars)
+  k.pair_stride = (PAIR_START_DOUBLES + WAVE * ppl * 4 + 2 * (WAVE * ppl * 5 + 16) + 15) / 16 * 16;
   HIP_TRY(hipMalloc(hdr, sizeof(int) * PAIR_HDR_INTS * (size_t)tiles));
   HIP_TRY(hipMalloc(buf, sizeof(double) * (size_t)k.pair_stride * tiles));
   k.pair_hdr = *hdr;

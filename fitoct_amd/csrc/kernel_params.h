@@ -138,7 +138,7 @@ struct KParams {
   // waves (nuts_device.hip "paired tiles"); the grid is 16 * ceil(pair_tiles / 8) blocks
   int pair;
   int pair_tiles;           // tiles of the launch (the tile map's entries)
-  int pair_stride;          // doubles per pair in pair_buf: start (4 vectors + 8) | record (5 + 16)
+  int pair_stride;          // doubles per pair in pair_buf: start (4 vectors + 8) | 2 records (5 + 16)
   int pair_test_absent;     // test hook (FITOCT_TEST_PAIR_ABSENT): partners leave at once
   int* pair_hdr;            // [pair_tiles][PAIR_HDR_INTS] hand-off words, zeroed per launch
   double* pair_buf;         // [pair_tiles][pair_stride]

@@ -130,12 +130,7 @@ struct ChainScalars {
   double pool_h[MAXDEPTH + 1], smp_h;
   // the running subtree's sum of the leaves' acceptance terms (added to sum_metro when the
   // subtree ends, so two-ended trajectories can sum per subtree and stay bitwise equal)
-  double sub_metro;
-  // two-ended trajectories, a producer's record of its last subtree (Chain::sub_publish):
-  // the sample's lp, sum r^2 and energy, the subtree's weight, acceptance sum; its weight's
-  // exponent, leaves, flags (SR_VALID / SR_DIVERGENT), depth; vectors: SR_* below
-  double r_slp, r_ss2, r_sh, r_twm, r_metro;
-  int r_twe, r_n, r_flags, r_depth;
+  double sub_metro, pad_sm;
   long long prof[2][32];   // diagnostic build: cycles and calls per action
 };
 static_assert(sizeof(ChainScalars) % 16 == 0, "LDS carve alignment");
@@ -883,9 +878,14 @@ struct Lds {
   // slots for the leaves it hands its booking helper (q, end-updated p, g, lp, sum r^2, depth,
   // leaf, transition)
   static constexpr int PX_BYTES = ((3 * VLEN + 8) * 8 + 15) / 16 * 16;
+  // ... and per end, two slots for its subtree records (Chain::rvec): 5 vectors, 16 scalars
+  // (one parameter per lane; at two, whose chain areas leave less room, one record slot per
+  // end in the producer's own area)
+  static constexpr int QX_DOUBLES = 5 * VLEN + 16;
+  static constexpr int QX_SLOTS = PPL == 1 ? 4 : 0;
   static __host__ __device__ constexpr int bytes(int G, int max_depth) {
     return head_bytes(G) + G * chain_bytes(max_depth) +
-           (G <= 2 ? G * HX_BYTES : G == 3 ? 4 * PX_BYTES : 0);
+           (G <= 2 ? G * HX_BYTES : G == 3 ? 4 * PX_BYTES + QX_SLOTS * QX_DOUBLES * 8 : 0);
   }
   AS_LDS char* base;
   int G, cb;
@@ -908,6 +908,10 @@ struct Lds {
   // producer s's hand-off slot k (two-ended trajectories, G = 3)
   __device__ AS_LDS double* px(int s, int k) const {
     return (AS_LDS double*)(base + head_bytes(G) + G * cb + (2 * s + k) * PX_BYTES);
+  }
+  // the record slots (end s, slot k = 2 s + k), after the hand-off slots
+  __device__ AS_LDS double* qx0() const {
+    return (AS_LDS double*)(base + head_bytes(G) + G * cb + 4 * PX_BYTES);
   }
 };
 
@@ -1101,7 +1105,7 @@ struct Chain {
   volatile AS_LDS int* bd = nullptr;
   RngKey key;
 
-  __device__ Chain(KPc& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
+  __device__ __forceinline__ Chain(KPc& P_, const Lds<PPL>& L, int slot_, int lc_, int lane_, int nct_)
       : pp(&P_), Sp(&L.cs(slot_)), Vb(L.vecs(slot_)), SUMS(L.sums(slot_)), AUX(L.aux(slot_)),
         LV(L.lvls(slot_)), RNG(L.lvls(slot_) + (size_t)P_.max_depth * NLVL * VLEN), MP(L.mp(slot_)),
         part(L.part()), Kinv(L.kinv()), bv(L.bv()),
@@ -1112,6 +1116,7 @@ struct Chain {
     helped = SPEC && !MIG && P_.G <= 2;
     deep = helped;
     HX = L.hx(L.G <= 2 ? slot_ : 0);
+    if (L.G == 3) QX0 = L.qx0();
     bidi = kTwoEnded && !MIG && deep && P_.bidi != 0;
     key = make_key(Pr().seed, (uint32_t)gid);
     if constexpr (KROW) {
@@ -2023,11 +2028,25 @@ struct Chain {
   // a transition takes about as long as its longer end, and the booking no longer paces it.
   enum SubRes : int { SL_MID = 0, SL_DONE = 1, SL_END = 2 };
   enum SubFlag : int { SR_VALID = 1, SR_DIVERGENT = 2 };
-  // a producer's subtree record, in vectors of its own chain area that a producer never uses:
-  // the proposal's q and g, the end's (last leaf's) momentum, the subtree's begin momentum and
-  // momentum sum; its scalars are ChainScalars::r_*
-  static constexpr int SR_SQ = V_SMP_Q, SR_SG = V_SMP_G, SR_EP = V_E1_P, SR_PB = V_E1_Q,
-                       SR_RHO = V_RHO, SR_NVEC = 5;
+  // A subtree record: RVEC vectors -- the proposal's q and g, the end's (last leaf's)
+  // momentum, the subtree's begin momentum and momentum sum -- and scalars RS_*.  Record m of
+  // end s sits in slot m % RSLOTS: in a tile of one chain two slots per end (Lds::qx0, after
+  // the hand-off slots), in a migrating tile (or at two parameters per lane) one, in vectors of
+  // the producer's own area that a producer never uses (V_E1_Q .. V_SMP_G; the scalars in
+  // V_RHO's).  Record m is written once the booking has taken record m - RSLOTS.
+  static constexpr int RVEC = 5, RSLOTS = (MIG || PPL > 1) ? 1 : 2;
+  enum RecVec : int { RV_SQ = 0, RV_SG, RV_EP, RV_PB, RV_RHO };
+  enum RecSc : int { RS_SLP = 0, RS_SS2, RS_SH, RS_TWM, RS_METRO, RS_TWE, RS_N, RS_FLAGS, RS_DEPTH,
+                     RS_N_ };
+  AS_LDS double* QX0 = nullptr;   // the tile's record slots (tiles of one chain)
+  __device__ __forceinline__ AS_LDS double* rvec(int s, int m) const {
+    if constexpr (RSLOTS == 1) return pvb(s) + V_E1_Q * VLEN;
+    else return QX0 + (size_t)(2 * s + (m & 1)) * Lds<PPL>::QX_DOUBLES;
+  }
+  __device__ __forceinline__ AS_LDS double* rsc(int s, int m) const {
+    if constexpr (RSLOTS == 1) return pvb(s) + V_RHO * VLEN;
+    else return rvec(s, m) + RVEC * VLEN;
+  }
   __device__ __forceinline__ V pld(const AS_LDS double* base, int v) const {
     V r;
 #pragma unroll
@@ -2080,32 +2099,32 @@ struct Chain {
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the record after its count
       const long long pt1 = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
-      const AS_LDS ChainScalars* R = psp(s);
-      const AS_LDS double* RV = pvb(s);
-      const int fl = uni(R->r_flags);
-      Sp->n_leapfrog = uni(Sp->n_leapfrog) + uni(R->r_n);
-      Sp->sum_metro = Sp->sum_metro + R->r_metro;
+      const AS_LDS double* RV = rvec(s, m);
+      const AS_LDS double* SC = rsc(s, m);
+      const int fl = uni((int)SC[RS_FLAGS]);
+      Sp->n_leapfrog = uni(Sp->n_leapfrog) + uni((int)SC[RS_N]);
+      Sp->sum_metro = Sp->sum_metro + SC[RS_METRO];
       if (fl & SR_DIVERGENT) Sp->divergent = 1;
       bool persist = false;
       if (fl & SR_VALID) {
         // top_merge: the sample, the trajectory's weight, the end, the depth
-        const XF Tw{R->r_twm, uni(R->r_twe)};
+        const XF Tw{SC[RS_TWM], uni((int)SC[RS_TWE])};
         const XF Ww{Sp->lsw_m, Sp->lsw_e};
         const double u_top = uniform(key, t, TAG_TOP, (uint32_t)d, 0u);
         const bool take = xf_gt(Tw, Ww) || xf_u_below(u_top, Tw, Ww);
         if (take) {
-          st(V_SMP_Q, pld(RV, SR_SQ));
-          st(V_SMP_G, pld(RV, SR_SG));
-          Sp->smp_lp = R->r_slp;
-          Sp->smp_s2 = R->r_ss2;
-          Sp->smp_h = R->r_sh;
+          st(V_SMP_Q, pld(RV, RV_SQ));
+          st(V_SMP_G, pld(RV, RV_SG));
+          Sp->smp_lp = SC[RS_SLP];
+          Sp->smp_s2 = SC[RS_SS2];
+          Sp->smp_h = SC[RS_SH];
         }
         const XF Wn = xf_add(Ww, Tw);
         Sp->lsw_m = Wn.m;
         Sp->lsw_e = Wn.e;
         Sp->depth = d + 1;
         // the trajectory-level U-turn checks (leaf_book's, at the subtree's last leaf)
-        const V pend = pld(RV, SR_EP), Tpb = pld(RV, SR_PB), Trho = pld(RV, SR_RHO);
+        const V pend = pld(RV, RV_EP), Tpb = pld(RV, RV_PB), Trho = pld(RV, RV_RHO);
         const int ef = s ? V_E1_P : V_E0_P;
         const V far = ld(s ? V_E0_P : V_E1_P), near = ld(ef), rho = ld(V_RHO);
         V rtot, rx, ry;
@@ -2255,11 +2274,15 @@ struct Chain {
     h_o = h;
     return SL_DONE;
   }
-  // the subtree's record for the booking (its slot free: the previous record was booked).
+  // record m of end s for the booking (its slot free: record m - RSLOTS was booked).
   // flags 0 / SR_DIVERGENT: an invalid subtree (only its counts matter)
-  __device__ __forceinline__ void sub_publish(const int flags, const XF Tw, const int Tprop, const V& Tpb,
-                              const V& Trho, const V& q, const V& pe, const V& g, const double lp,
-                              const double s2, const double h) {
+  __device__ __forceinline__ void sub_publish(const int s, const int m, const int flags,
+                                              const XF Tw, const int Tprop, const V& Tpb,
+                                              const V& Trho, const V& q, const V& pe,
+                                              const V& g, const double lp, const double s2,
+                                              const double h) {
+    AS_LDS double* const RV = rvec(s, m);
+    AS_LDS double* const SC = rsc(s, m);
     if (flags & SR_VALID) {
       V sq = q, sg = g;
       double slp = lp, ss2 = s2, sh = h;
@@ -2267,32 +2290,35 @@ struct Chain {
         const AS_GLB double* pq = pslot(Tprop, P_Q);
         const AS_GLB double* pg = pslot(Tprop, P_G);
 #pragma unroll
-        for (int s = 0; s < PPL; ++s) {
-          sq.a[s] = ok(s) ? pq[idx(s)] : 0.0;
-          sg.a[s] = ok(s) ? pg[idx(s)] : 0.0;
+        for (int k = 0; k < PPL; ++k) {
+          sq.a[k] = ok(k) ? pq[idx(k)] : 0.0;
+          sg.a[k] = ok(k) ? pg[idx(k)] : 0.0;
         }
         slp = Sp->pool_lp[Tprop];
         ss2 = Sp->pool_s2[Tprop];
         sh = Sp->pool_h[Tprop];
       }
-      st(SR_SQ, sq);
-      st(SR_SG, sg);
-      st(SR_EP, pe);
-      st(SR_PB, Tpb);
-      st(SR_RHO, Trho);
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) {
+        RV[RV_SQ * VLEN + idx(k)] = sq.a[k];
+        RV[RV_SG * VLEN + idx(k)] = sg.a[k];
+        RV[RV_EP * VLEN + idx(k)] = pe.a[k];
+        RV[RV_PB * VLEN + idx(k)] = Tpb.a[k];
+        RV[RV_RHO * VLEN + idx(k)] = Trho.a[k];
+      }
       if (lane == 0) {
-        Sp->r_slp = slp;
-        Sp->r_ss2 = ss2;
-        Sp->r_sh = sh;
-        Sp->r_twm = Tw.m;
-        Sp->r_twe = Tw.e;
+        SC[RS_SLP] = slp;
+        SC[RS_SS2] = ss2;
+        SC[RS_SH] = sh;
+        SC[RS_TWM] = Tw.m;
+        SC[RS_TWE] = (double)Tw.e;
       }
     }
     if (lane == 0) {
-      Sp->r_metro = Sp->sub_metro;
-      Sp->r_n = Sp->n_leapfrog;
-      Sp->r_flags = flags;
-      Sp->r_depth = Sp->depth;
+      SC[RS_METRO] = Sp->sub_metro;
+      SC[RS_N] = (double)Sp->n_leapfrog;
+      SC[RS_FLAGS] = (double)flags;
+      SC[RS_DEPTH] = (double)Sp->depth;
     }
   }
 
@@ -2950,11 +2976,14 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane, volatil
 // chain, its helper and the backward end's producer; 1: its partner, which grows the forward
 // end on its own gradient waves.  Blocks b and b + 8 (one XCD when blocks are dealt round-robin
 // over the 8 XCDs; for speed only, the hand-off is correct on any placement) form a pair.
-template <class R, int BPT, int NNP, int PPL, int MODE, int FAM, bool MIG, bool SPEC>
+// PAIR: the paired launch (one-chain tiles with two-ended trajectories and partners; MIG =
+// false, SPEC = true): its own instantiation, so that neither the bridges nor the partner's
+// roles cost the unpaired kernels registers
+template <class R, int BPT, int NNP, int PPL, int MODE, int FAM, bool MIG, bool SPEC, bool PAIR>
 __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict__ Pg,
                                                       const int* __restrict__ tile_map) {
   int tix = blockIdx.x, role = 0;
-  if (SPEC && !MIG && ((KPc*)Pg)->pair) {   // (Pg[0]: every problem of a batch pairs alike)
+  if constexpr (PAIR) {
     role = (tix >> 3) & 1;
     tix = ((tix >> 4) << 3) | (tix & 7);
     if (tix >= ((KPc*)Pg)->pair_tiles) return;   // the grid's padding to whole groups of 16
@@ -2992,7 +3021,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   __shared__ int live_chains;   // chains the tile hosts (speculation policy, Chain::live)
   // paired tiles: this pair's hand-off words and buffer; pair_on: the partner has joined
   // (partner tile: 1 = it grows the forward end, 0 = it leaves at once)
-  const bool paired = SPEC && !MIG && bidi && P.pair != 0;
+  const bool paired = PAIR && bidi;
   AS_GLB int* const xh = paired ? (AS_GLB int*)P.pair_hdr + (size_t)tix * PAIR_HDR_INTS : nullptr;
   AS_GLB double* const xb = paired ? (AS_GLB double*)P.pair_buf + (size_t)tix * P.pair_stride : nullptr;
   __shared__ int pair_on;
@@ -3164,10 +3193,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     // the one booked, and publishes one record per subtree once the booking has taken the
     // previous one.  `epoch`: the slot's sweeps so far (grad_cnt[slot] counts NGW per sweep).
     // Ends with BD_GEN < 0 (the tile's chain finished) or, in a migrating tile, with the launch.
-    // helped: a helper wave books this end's leaves (nuts_device.hip serve; tiles of one chain),
-    // else the producer books them itself (a migrating launch's tail)
-    constexpr bool helped = !MIG;
     auto produce = [&](const int s, const int slot, long long epoch) {
+      // helped: a helper wave books this end's leaves (serve: tiles of one chain -- the backward
+      // end, and in a paired launch the forward end too), else the producer books them itself
+      // (the forward end in an unpaired tile, a migrating launch's tail)
+      const bool helped = !MIG && (s == 0 || PAIR);
       int hreq = 0;   // leaves handed to the helper
       Ch pr(P, L, slot, c0, lane, nct);
       pr.bd = (volatile AS_LDS int*)bd;
@@ -3264,13 +3294,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             __builtin_amdgcn_s_sleep(1);
           }
         };
-        // the record slot is free once the booking has taken records 0 .. m - 1
+        // record m's slot is free once the booking has taken record m - RSLOTS
         auto wait_room = [&](const int m) -> bool {   // false: the tree ended
           Patience w;
           const long long pt = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
           for (;;) {
             if (lds_load(&bd[BD_GEN]) != g) return false;
-            if (lds_load(&bd[BD_CONS + s]) >= m) {
+            if (lds_load(&bd[BD_CONS + s]) >= m - Ch::RSLOTS + 1) {
               if (kProfile) pf_may += (long long)__builtin_amdgcn_s_memtime() - pt;
               return true;
             }
@@ -3399,7 +3429,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             if (!wait_room(m)) break;
             const int fl = r == Ch::SL_DONE ? Ch::SR_VALID
                                             : pr.uni(pr.Sp->divergent) ? Ch::SR_DIVERGENT : 0;
-            pr.sub_publish(fl, Tw, Tprop, Tpb, Trho, qn, pe, gn, lp, s2, h);
+            pr.sub_publish(s, m, fl, Tw, Tprop, Tpb, Trho, qn, pe, gn, lp, s2, h);
             wave_publish();   // the record lands before its count
             ++m;
             if (lane == 0) __atomic_store_n(&bd[BD_PROD + s], (g << 16) | m, __ATOMIC_RELAXED);
@@ -3471,7 +3501,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if (r != Ch::SL_MID) {   // the subtree ended: its record, once the slot is free
           Patience w;
           bool room = true;
-          while (lds_load(&bd[BD_CONS + s]) < hm) {
+          while (lds_load(&bd[BD_CONS + s]) < hm - Ch::RSLOTS + 1) {
             if (lds_load(&bd[BD_GEN]) != gen || w.expired(2 * MIG_WAIT_TICKS)) {
               room = false;
               break;
@@ -3481,7 +3511,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           if (room) {
             const int fl = r == Ch::SL_DONE ? Ch::SR_VALID
                                             : hc.uni(hc.Sp->divergent) ? Ch::SR_DIVERGENT : 0;
-            hc.sub_publish(fl, Tw, Tprop, Tpb, Trho, q, pe, gg, lp, s2, h);
+            hc.sub_publish(s, hm, fl, Tw, Tprop, Tpb, Trho, q, pe, gg, lp, s2, h);
             wave_publish();   // the record lands before its count
             ++hm;
             if (lane == 0) __atomic_store_n(&bd[BD_PROD + s], (gen << 16) | hm, __ATOMIC_RELAXED);
@@ -3519,12 +3549,20 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     // m only once the (mirrored, never larger) count of records booked is m, so one count
     // guards the record's three slots.  Counts and the booked depth carry their transition
     // (gen << 16) and only grow within it.
-    constexpr int RV = Ch::SR_NVEC;   // record vectors; then 16 scalars
-    auto rvec = [](const int v) {      // the record's v-th vector in a chain area
-      return v == 0 ? Ch::SR_SQ : v == 1 ? Ch::SR_SG : v == 2 ? Ch::SR_EP : v == 3 ? Ch::SR_PB : Ch::SR_RHO;
-    };
+    constexpr int QXD = Lds<PPL>::QX_DOUBLES;   // a record: Ch::RVEC vectors, then scalars
+    constexpr int RVD = Ch::RVEC * Ch::VLEN;
     auto pair_start = [&]() { return xb; };
-    auto pair_rec = [&]() { return xb + 4 * Ch::VLEN + PAIR_START_DOUBLES; };
+    // the pair's record slot k (the forward end's records m, k = m % 2): vectors, scalars
+    auto pair_rec = [&](const int k) { return xb + 4 * Ch::VLEN + PAIR_START_DOUBLES + k * QXD; };
+    // end 1's record slot k in this tile (Chain::rvec / rsc)
+    auto fwd_vec = [&](const int k) -> AS_LDS double* {
+      if constexpr (Ch::RSLOTS == 1) return L.vecs(2) + V_E1_Q * Ch::VLEN;
+      else return L.qx0() + (2 + k) * QXD;
+    };
+    auto fwd_sc = [&](const int k) -> AS_LDS double* {
+      if constexpr (Ch::RSLOTS == 1) return L.vecs(2) + V_RHO * Ch::VLEN;
+      else return fwd_vec(k) + RVD;
+    };
     auto bridge_in = [&]() -> bool {   // false: the pair did not form (grow the end here)
       {
         Patience w;   // the chain's first transition (or its end)
@@ -3543,7 +3581,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       if ((st & PS_LOCAL) || !(st & PS_JOIN)) return false;
       constexpr int VL = Ch::VLEN;
       AS_GLB double* const xs = pair_start();
-      AS_GLB double* const xr = pair_rec();
+
       AS_LDS double* const av = L.vecs(2);        // producer area 2: the start, the record
       AS_LDS ChainScalars* const as = &L.cs(2);
       const volatile AS_LDS int* depth = (const volatile AS_LDS int*)&L.cs(0).depth;
@@ -3596,27 +3634,19 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         // the partner's next record of this transition
         const int pc = __builtin_amdgcn_readfirstlane(x_ldi(xh + PH_COUNT));
         if ((pc >> 16) == seen && (pc & 0xFFFF) > copied) {
-#pragma unroll
-          for (int v = 0; v < RV; ++v)
-#pragma unroll
-            for (int s = 0; s < PPL; ++s) {
-              const int k = s * WAVE + lane;
-              av[rvec(v) * VL + k] = x_ld(xr + v * VL + k);
+          const int cnt = pc & 0xFFFF;
+          for (int n = copied; n < cnt; ++n) {   // records n: the pair's slot -> end 1's slot
+            const AS_GLB double* src = pair_rec(n & 1);
+            AS_LDS double* dv = fwd_vec(n & 1);
+            AS_LDS double* ds = fwd_sc(n & 1);
+            for (int i = lane; i < QXD; i += WAVE) {
+              const double v = x_ld(src + i);
+              if (i < RVD) dv[i] = v;
+              else ds[i - RVD] = v;
             }
-          if (lane == 0) {
-            const AS_GLB double* sc = xr + RV * VL;
-            as->r_slp = x_ld(sc);
-            as->r_ss2 = x_ld(sc + 1);
-            as->r_sh = x_ld(sc + 2);
-            as->r_twm = x_ld(sc + 3);
-            as->r_metro = x_ld(sc + 4);
-            as->r_twe = (int)x_ld(sc + 5);
-            as->r_n = (int)x_ld(sc + 6);
-            as->r_flags = (int)x_ld(sc + 7);
-            as->r_depth = (int)x_ld(sc + 8);
           }
-          wave_publish();   // the record lands before its count
-          copied = pc & 0xFFFF;
+          wave_publish();   // the records land before their count
+          copied = cnt;
           if (lane == 0) __atomic_store_n(&bd[BD_PROD + 1], (seen << 16) | copied, __ATOMIC_RELAXED);
           idle = Patience{};
           continue;
@@ -3630,7 +3660,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     auto bridge_out = [&]() {
       constexpr int VL = Ch::VLEN;
       AS_GLB double* const xs = pair_start();
-      AS_GLB double* const xr = pair_rec();
+
       AS_LDS double* const av = L.vecs(2);        // the producer's area
       AS_LDS ChainScalars* const as = &L.cs(2);
       volatile AS_LDS int* depth = (volatile AS_LDS int*)&L.cs(0).depth;   // the producer's S0
@@ -3677,28 +3707,16 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         }
         const int pw = lds_load(&bd[BD_PROD + 1]);
         if ((pw >> 16) == seen && (pw & 0xFFFF) > copied) {
-          wave_fence();   // the record after its count
-#pragma unroll
-          for (int v = 0; v < RV; ++v)
-#pragma unroll
-            for (int s = 0; s < PPL; ++s) {
-              const int k = s * WAVE + lane;
-              x_st(xr + v * VL + k, av[rvec(v) * VL + k]);
-            }
-          if (lane == 0) {
-            AS_GLB double* sc = xr + RV * VL;
-            x_st(sc, as->r_slp);
-            x_st(sc + 1, as->r_ss2);
-            x_st(sc + 2, as->r_sh);
-            x_st(sc + 3, as->r_twm);
-            x_st(sc + 4, as->r_metro);
-            x_st(sc + 5, (double)as->r_twe);
-            x_st(sc + 6, (double)as->r_n);
-            x_st(sc + 7, (double)as->r_flags);
-            x_st(sc + 8, (double)as->r_depth);
+          const int cnt = pw & 0xFFFF;
+          wave_fence();   // the records after their count
+          for (int n = copied; n < cnt; ++n) {   // records n: end 1's slot -> the pair's slot
+            const AS_LDS double* sv = fwd_vec(n & 1);
+            const AS_LDS double* ss = fwd_sc(n & 1);
+            AS_GLB double* dst = pair_rec(n & 1);
+            for (int i = lane; i < QXD; i += WAVE) x_st(dst + i, i < RVD ? sv[i] : ss[i - RVD]);
           }
-          x_drain();   // the record has reached memory before its count
-          copied = pw & 0xFFFF;
+          x_drain();   // the records have reached memory before their count
+          copied = cnt;
           if (lane == 0) x_sti(xh + PH_COUNT, (seen << 16) | copied);
           idle = Patience{};
           continue;
@@ -3715,18 +3733,25 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       wave_fence();
       if (lane == 0) atomicSub(&n_active, 1);
     };
-    if constexpr (SPEC && !MIG) {
+    if constexpr (PAIR) {
       if (role == 1 && pair_on && c == 2) bridge_out();   // partner tile: the bridge
-      if (bidi && c == 1 && (role == 0 || pair_on)) {   // the booking helper of the producers
+    }
+    if constexpr (SPEC && !MIG) {
+      if (bidi && c == 1 && (role == 0 || pair_on)) {
+        // the booking helper of producer 0 (a primary; in a paired launch also its producer 1
+        // if the pair did not form) or 1 (a partner).  An unpaired launch's producer 1 books
+        // its leaves itself (a helper serving both ends would pace both).
+        constexpr bool both = PAIR;
         Patience w;
-        for (int s = 0;; s ^= 1) {   // (one call site: serve is inlined once)
+        for (int s = role;; s = (both && role == 0) ? s ^ 1 : s) {   // (one call site of serve)
           const int a = serve(s);
           if (a > 0) {
             w = Patience{};
             continue;
           }
-          if (a < 0 && lds_load(&help_req[s ^ 1]) < 0) break;   // both producers gone
-          if (s == 1) {
+          const bool alt = both && role == 0;
+          if (a < 0 && (!alt || lds_load(&help_req[s ^ 1]) < 0)) break;   // producers gone
+          if (!alt || s == 1) {
             if (w.expired(MIG_WAIT_TICKS)) break;   // never, short of a fault
             __builtin_amdgcn_s_sleep(1);
           }
@@ -3738,8 +3763,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     // wave 3 is the bridge.  (One call site: produce is inlined once.)
     if (bidi && c >= 2 && (role == 0 || (pair_on && c == 3))) {
       bool here = true;
-      if constexpr (SPEC && !MIG) {
-        if (paired && role == 0 && c == 3) here = !bridge_in();
+      if constexpr (PAIR) {
+        if (role == 0 && c == 3) here = !bridge_in();
       }
       if (here) produce(c - 2, c - 1, 0);
       wave_fence();
@@ -4119,10 +4144,11 @@ static hipError_t launch_t(bool logp, const KParams& P, const KParams* dP, int t
     // three samplers: with migration, with speculative leaves (one chain per tile), plain
     // four samplers: with / without migration, with / without speculative leaves
     auto k = P.mig != nullptr
-                 ? (P.spec ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, true, true>
-                           : nuts_kernel<R, BPT, NNP, PPL, MODE, F, true, false>)
-             : P.spec ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, false, true>
-                      : nuts_kernel<R, BPT, NNP, PPL, MODE, F, false, false>;
+                 ? (P.spec ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, true, true, false>
+                           : nuts_kernel<R, BPT, NNP, PPL, MODE, F, true, false, false>)
+             : P.spec ? (P.pair ? nuts_kernel<R, BPT, NNP, PPL, MODE, F, false, true, true>
+                                : nuts_kernel<R, BPT, NNP, PPL, MODE, F, false, true, false>)
+                      : nuts_kernel<R, BPT, NNP, PPL, MODE, F, false, false, false>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(k, dim3(tiles), dim3(TPB), lds, st, dP, tile_map);
   }

@@ -11,9 +11,10 @@ asserts 0 VGPR spill and 0 scratch for each instantiation below.  If the record 
 or older than the kernel source, the family is recompiled device-only for the remarks.
 
 Template arguments of ``nuts_kernel``: <R, BPT (bins per lane), NNP, PPL, MODE, FAM,
-MIG (chain migration), SPEC (speculative leaves)>; the plan picks them in
-``fitoct_api.cpp`` (tiles of one chain -> MIG = false, SPEC = true; 1024 chains on 256 CUs
--> G = 4, migration + tail speculation; batch mode -> MIG = false, SPEC = false).
+MIG (chain migration), SPEC (speculative leaves), PAIR (paired tiles)>; the plan picks them
+in ``fitoct_api.cpp`` (tiles of one chain -> MIG = false, SPEC = true, and PAIR = true when
+twice the tiles fit on the chip; 1024 chains on 256 CUs -> G = 4, migration + tail
+speculation; batch mode -> MIG = false, SPEC = false).
 """
 import os
 import subprocess
@@ -28,9 +29,9 @@ from fitoct_amd import build as B  # noqa: E402
 FAM_OBJ = {0: "nuts_normal", 1: "nuts_lasso", 2: "nuts_horseshoe", 3: "nuts_monoexp"}
 
 
-def mangled(bpt, fam, mig, spec, nnp=15, ppl=1, mode=0, real="d"):
+def mangled(bpt, fam, mig, spec, pair=False, nnp=15, ppl=1, mode=0, real="d"):
     return (f"_ZN6fitoct11nuts_kernelI{real}Li{bpt}ELi{nnp}ELi{ppl}ELi{mode}ELi{fam}E"
-            f"Lb{int(mig)}ELb{int(spec)}EEEvPKNS_7KParamsEPKi")
+            f"Lb{int(mig)}ELb{int(spec)}ELb{int(pair)}EEEvPKNS_7KParamsEPKi")
 
 
 # (BASELINE config, family, kernel)
@@ -40,10 +41,12 @@ LAUNCHED = [
     ("config 3 without speculation (FITOCT_NO_SPEC)", 2, mangled(8, 2, True, False)),
     ("config 4: lasso N=4096, 16 bins per lane, migrating + tail speculation",
      1, mangled(16, 1, True, True)),
-    ("config 2: normal N=512, 128 chains, tiles of one chain (two-ended trajectories)",
-     0, mangled(2, 0, False, True)),
+    ("config 2: normal N=512, 128 chains, paired tiles of one chain (two-ended trajectories)",
+     0, mangled(2, 0, False, True, True)),
+    ("config 2 unpaired (FITOCT_NO_PAIR; 129..256 one-chain tiles)", 0, mangled(2, 0, False, True)),
     ("config 5 at one GPU: batch tiles of four chains, plain sampler", 0, mangled(2, 0, False, False)),
-    ("config 5 multi-GPU shares: batch tiles of one chain (speculating)", 0, mangled(2, 0, False, True)),
+    ("config 5 8-GPU share: paired batch tiles of one chain", 0, mangled(2, 0, False, True, True)),
+    ("config 5 4-GPU share: batch tiles of one chain (speculating)", 0, mangled(2, 0, False, True)),
 ]
 
 
@@ -108,14 +111,14 @@ def test_every_resident_bin_instantiation_keeps_the_chain_in_registers(fam):
     rows = _rows(fam)
     seen = 0
     for bpt in (1, 2, 4, 8, 16):
-        for mig in (False, True):
-            for spec in (False, True):
-                k = mangled(bpt, fam, mig, spec)
-                assert k in rows, k
-                r = rows[k]
-                if (fam, mig, spec) == (0, True, True):
-                    assert r.get("VGPRs Spill", 99) <= 4 and r.get("ScratchSize", 99) <= 20, (k, r)
-                else:
-                    assert r.get("VGPRs Spill", -1) == 0 and r.get("ScratchSize", -1) == 0, (k, r)
-                seen += 1
-    assert seen == 20
+        for mig, spec, pair in ((False, False, False), (False, True, False), (False, True, True),
+                                (True, False, False), (True, True, False)):
+            k = mangled(bpt, fam, mig, spec, pair)
+            assert k in rows, k
+            r = rows[k]
+            if (fam, mig, spec) == (0, True, True):
+                assert r.get("VGPRs Spill", 99) <= 4 and r.get("ScratchSize", 99) <= 20, (k, r)
+            else:
+                assert r.get("VGPRs Spill", -1) == 0 and r.get("ScratchSize", -1) == 0, (k, r)
+            seen += 1
+    assert seen == 25
