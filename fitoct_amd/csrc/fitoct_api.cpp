@@ -1128,9 +1128,20 @@ int32_t fitoct_plan_wait(fitoct_plan* pl) {
         for (int s = 0; s < 2; ++s)
           fprintf(stderr,
                   "[fitoct stamps] producer of end %d per produced leaf: waiting for its sweep %.0f, "
-                  "for lookahead / ring room %.0f, in trees %.0f (leaves per tile %.0f)\n",
+                  "for lookahead / record slot %.0f, in trees %.0f (leaves per tile %.0f)\n",
                   s, pe[s][0] / std::max(pe[s][2], 1.0), pe[s][1] / std::max(pe[s][2], 1.0),
                   pe[s][3] / std::max(pe[s][2], 1.0), pe[s][2] / pl->tiles);
+        double hb2[2] = {0, 0}, hn2[2] = {0, 0};
+        for (int t = 0; t < pl->tiles; ++t)
+          for (int r = 0; r < 2; ++r) {
+            hb2[r] += h[(size_t)NSTAMP * t + 96 + 2 * r];
+            hn2[r] += h[(size_t)NSTAMP * t + 97 + 2 * r];
+          }
+        for (int r = 0; r < 2; ++r)
+          if (hn2[r] > 0)
+            fprintf(stderr,
+                    "[fitoct stamps] booking helper (%s tile): %.0f cycles per booked leaf, %.0f "
+                    "leaves per tile\n", r ? "partner" : "primary", hb2[r] / hn2[r], hn2[r] / pl->tiles);
       }
     }
     pl->ran = true;

@@ -3742,10 +3742,21 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         // if the pair did not form) or 1 (a partner).  An unpaired launch's producer 1 books
         // its leaves itself (a helper serving both ends would pace both).
         constexpr bool both = PAIR;
+        // below the producers and the sweep's NUTS neighbours: it has slack (4.1 k of a
+        // producer's 5.8 k cycles per leaf, profiling build), and the gradient wave sharing its
+        // SIMD is on a sweep's critical path (config 2: priority 2 / 1 +0.5 % over 3,
+        // profiles/r06_ab_prio.txt)
+        __builtin_amdgcn_s_setprio(2);
         Patience w;
+        long long pf_busy = 0, pf_n = 0;   // profiling build: cycles booking, leaves booked
         for (int s = role;; s = (both && role == 0) ? s ^ 1 : s) {   // (one call site of serve)
+          const long long pt = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
           const int a = serve(s);
           if (a > 0) {
+            if (kProfile) {
+              pf_busy += (long long)__builtin_amdgcn_s_memtime() - pt;
+              ++pf_n;
+            }
             w = Patience{};
             continue;
           }
@@ -3755,6 +3766,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             if (w.expired(MIG_WAIT_TICKS)) break;   // never, short of a fault
             __builtin_amdgcn_s_sleep(1);
           }
+        }
+        if (kProfile && P.stamps != nullptr && lane == 0) {   // this tile's booking helper
+          AS_GLB long long* o = (AS_GLB long long*)P.stamps + (size_t)tix * NSTAMP + 96 + 2 * role;
+          o[0] = pf_busy;
+          o[1] = pf_n;
         }
       }
     }
