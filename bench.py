@@ -107,25 +107,49 @@ def host_cpu_info():
     except OSError:
         pass
     sockets = set()
+    cores = {}   # logical CPU -> (socket, core): SMT siblings share a physical core
     try:
         with open("/proc/cpuinfo") as f:
+            cpu = sock = None
             for ln in f:
-                if ln.startswith("physical id"):
-                    sockets.add(ln.split(":", 1)[1].strip())
-    except OSError:
+                k, _, v = ln.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "processor":
+                    cpu = int(v)
+                elif k == "physical id":
+                    sock = v
+                    sockets.add(v)
+                elif k == "core id" and cpu is not None:
+                    cores[cpu] = (sock, v)
+    except (OSError, ValueError):
         pass
     share = min(avail, quota) if quota else avail
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = list(range(node))
+    node_phys = len(set(cores.values())) or None
+    aff_phys = len({cores[c] for c in aff if c in cores}) or None
     return {"node_cpus": node, "affinity_cpus": avail, "cgroup_quota_cpus": quota,
-            "share_cpus": share, "sockets": len(sockets) or None, "model": model}
+            "share_cpus": share, "sockets": len(sockets) or None, "model": model,
+            # SMT: the node's physical cores and the physical cores the affinity mask spans
+            # (a quota of share_cpus logical CPUs may run on fewer cores than CPUs)
+            "node_physical_cores": node_phys, "affinity_physical_cores": aff_phys,
+            "smt_threads_per_core": (round(node / node_phys, 2) if node_phys else None)}
 
 
-def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, adapt_delta=0.8, max_treedepth=10):
+def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, adapt_delta=0.8, max_treedepth=10,
+                 same_length=None):
     """C oracle (oracle/fitoct_oracle.c, OpenMP over chains): a bounded run of the
     same problem, one chain per host thread (250 warmup + 250 draws, ~10-20 s), its
     leapfrog rate scaled by the GPU step's leapfrogs per draw.  It runs on every CPU
     this job may use (affinity and cgroup quota: the job's share of a shared node);
     chains are independent, so the node-wide rate is also given as the measured
-    per-thread rate times the node's logical CPUs (``value_node_est``)."""
+    per-thread rate times the node's logical CPUs (``value_node_est``).
+
+    ``same_length`` = (W, S): also a direct run at the workload's own per-chain length --
+    one chain per thread of the share, W warmup + S draws each, value = chains x S / wall,
+    no scaling (``value_measured_same_length``)."""
     from oracle import nuts_c
     hw = host_cpu_info()
     threads = hw["share_cpus"]
@@ -138,7 +162,21 @@ def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, adapt_delta=0.8, max_tre
     lf_rate = lf / wall
     value = draws_per_step * lf_rate / gpu_lf_per_step
     post = o["draws"][:, W:, :] if cfg.save_warmup else o["draws"]
+    direct = {}
+    if same_length is not None:
+        W2, S2 = same_length
+        cfg2 = make_config(8, threads, 950_000, 0, W2, S2, adapt_delta, max_treedepth)
+        t2 = time.perf_counter()
+        nuts_c.sample(prob, cfg2, nthreads=threads)
+        wall2 = time.perf_counter() - t2
+        v2 = threads * S2 / wall2
+        direct = {"value_measured_same_length": round(v2, 2),
+                  "same_length_sample": (f"C oracle NUTS, {threads} chains x ({W2} warmup + {S2} "
+                                         f"draws) on {threads} threads, {wall2:.1f} s: chains x "
+                                         f"draws / wall, no scaling"),
+                  "measured_over_scaled": round(v2 / value, 3)}
     return {"means": np.nanmean(post, axis=(0, 1)), "lf_rate": lf_rate, "value": value,
+            **direct,
             "unit": "draws/s",
             "cores": threads, "kind": "port",
             "value_node_est": value * hw["node_cpus"] / threads,
@@ -358,11 +396,17 @@ def main():
     draws_step = world * C_plan * S_it
     value = draws_step / (ms_per_step / 1e3)
 
-    # convergence of the last step (rank 0's chains): split R-hat over parameters
+    # convergence of the last step: split R-hat over parameters, over every rank's chains (the
+    # gathered draws: rank 0 holds the whole job's last step after its gather)
     last = outs[-1].draws
     cols = prob.column_names()
     W_saved = outs[-1].warmup_saved
-    conv = convergence(last, W_saved, cols)
+    conv_draws = last
+    if world > 1 and rank == 0 and "gather" in bufs:
+        shp = last.shape
+        conv_draws = np.concatenate([g.cpu().numpy().reshape(shp) for g in bufs["gather"]])
+    conv = convergence(conv_draws, W_saved, cols)
+    conv["rhat_chains"] = int(conv_draws.shape[0])
     lf_per_draw = float(np.mean(lf_steps)) / (C_plan * (W_it + S_it))
 
     workload = (f"fitExpGP+{conf['prior']} N={N_bins} Nn={NN} {C} chains/GPU "
@@ -410,7 +454,7 @@ def main():
     }
     if rank == 0 and n_units == 1 and not args.no_cpu:
         cb = cpu_baseline(prob, float(np.mean(lf_steps)), C * S_it, args.adapt_delta,
-                          args.max_treedepth)
+                          args.max_treedepth, same_length=(W_it, S_it))
         o_means = cb.pop("means")
         line["cpu_baseline"] = cb
         # north star: posterior means within 1 % of the CPU path on the same inputs.
