@@ -167,14 +167,21 @@ def cpu_baseline(prob, gpu_lf_per_step, draws_per_step, adapt_delta=0.8, max_tre
         W2, S2 = same_length
         cfg2 = make_config(8, threads, 950_000, 0, W2, S2, adapt_delta, max_treedepth)
         t2 = time.perf_counter()
-        nuts_c.sample(prob, cfg2, nthreads=threads)
+        o2 = nuts_c.sample(prob, cfg2, nthreads=threads)
         wall2 = time.perf_counter() - t2
         v2 = threads * S2 / wall2
+        lf2 = float(o2["leapfrogs"].sum())
         direct = {"value_measured_same_length": round(v2, 2),
                   "same_length_sample": (f"C oracle NUTS, {threads} chains x ({W2} warmup + {S2} "
                                          f"draws) on {threads} threads, {wall2:.1f} s: chains x "
                                          f"draws / wall, no scaling"),
-                  "measured_over_scaled": round(v2 / value, 3)}
+                  "measured_over_scaled": round(v2 / value, 3),
+                  # the ratio's two factors: the gradient rate of the longer run over the
+                  # sample's (the same problem on the same threads: ~1) and the GPU step's
+                  # gradients per draw over this run's own (its 16 chains' tree depths)
+                  "same_length_grad_rate_ratio": round(lf2 / wall2 / lf_rate, 3),
+                  "same_length_grads_per_draw_ratio": round(
+                      (gpu_lf_per_step / draws_per_step) / (lf2 / (threads * S2)), 3)}
     return {"means": np.nanmean(post, axis=(0, 1)), "lf_rate": lf_rate, "value": value,
             **direct,
             "unit": "draws/s",
