@@ -342,8 +342,7 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   } else if (pl->mixed) {
     mode = MODE_ROWS;
   } else {
-    const bool poly = !p->B && getenv("FITOCT_NO_POLY") == nullptr &&
-                      build_poly(p, B, pl->nnp, ta, kinv, bv);
+    const bool poly = !p->B && build_poly(p, B, pl->nnp, ta, kinv, bv);
     mode = poly ? MODE_POLY : MODE_ROWS;
   }
   // f64 rows (NNP doubles per bin) are always streamed
@@ -353,7 +352,7 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   // layout (y, 1/uy, a in registers; c*x and t formed from the lane's first bin)
   double R16[24];
   if (mode == MODE_POLY && !mono && !pl->mixed && pl->bpt == 0 && p->N <= 16 * GT &&
-      force_bpt < 0 && getenv("FITOCT_NO_GEO") == nullptr && getenv("FITOCT_NO_BPT16") == nullptr &&
+      force_bpt < 0 && getenv("FITOCT_NO_GEO") == nullptr &&
       geo_ratios(p, pl->nnp, 16, R16)) {
     pl->bpt = 16;
     n_pad = 16 * GT;

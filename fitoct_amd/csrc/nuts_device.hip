@@ -4206,12 +4206,8 @@ hipError_t FITOCT_CAT(launch_family_, FITOCT_FAMILY)(bool logp, bool mixed, int 
                                                      const KParams& P, const KParams* dP,
                                                      int tiles, hipStream_t st,
                                                      const int* tile_map) {
-#ifdef FITOCT_ONE_VARIANT
-  return launch_t<double, 8, 15, 1, MODE_POLY>(logp, P, dP, tiles, st, tile_map);
-#else
   if (nnp == 15) return launch_n<15, 1>(logp, mixed, bpt, P, dP, tiles, st, tile_map);
   return launch_n<24, 2>(logp, mixed, bpt, P, dP, tiles, st, tile_map);
-#endif
 }
 
 }  // namespace fitoct
