@@ -76,7 +76,7 @@ class PlanInfo(C.Structure):
         ("lds_bytes", C.c_int32), ("n_pad", C.c_int32), ("draws_bytes", C.c_int64),
         ("sampler", C.c_int32), ("n_devices", C.c_int32),
         ("two_ended", C.c_int32), ("ring_records", C.c_int32), ("ring_records_in_levels", C.c_int32),
-        ("paired", C.c_int32), ("workgroups", C.c_int32),
+        ("paired", C.c_int32), ("workgroups", C.c_int32), ("basis_mode", C.c_int32),
     ]
 
 
@@ -205,7 +205,7 @@ def _single_hip_runtime():
         pass
 
 
-ABI_VERSION = 7   # include/fitoct.h FITOCT_ABI_VERSION
+ABI_VERSION = 8   # include/fitoct.h FITOCT_ABI_VERSION
 
 
 def lib():

@@ -299,7 +299,7 @@ void stage(const fitoct_problem* p, const std::vector<double>& B, const std::vec
 
 // common planning for the sampler and the logp kernel
 int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precision, int device,
-                int max_depth, int g_chains = 0, int force_bpt = -1) {
+                int max_depth, int g_chains = 0, int force_bpt = -1, bool poly_only = false) {
   int rc = check_problem(p);
   if (rc) return rc;
   int ndev = 0;
@@ -333,6 +333,7 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   // basis mode (see kernel_params.h BasisMode)
   std::vector<double> ta, kinv, bv;
   int mode;
+  bool rows_res = false;
   if (mono && !pl->mixed) {
     mode = MODE_POLY;
     ta.assign(2 * (size_t)p->N, 0.0);
@@ -342,12 +343,16 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
   } else if (pl->mixed) {
     mode = MODE_ROWS;
   } else {
-    const bool poly = !p->B && build_poly(p, B, pl->nnp, ta, kinv, bv);
+    // N <= 512 (configs 2 and 5): the basis rows themselves, 1-2 bins of 15 doubles per lane
+    // in the gradient waves' registers -- the sampler's leaf then has no K^-1 products
+    // (write_mp, finish_grad) on its critical path.  Wider problems: the factorised basis.
+    rows_res = !poly_only && p->N <= 2 * GT && pl->nnp == 15;
+    const bool poly = !rows_res && !p->B && build_poly(p, B, pl->nnp, ta, kinv, bv);
     mode = poly ? MODE_POLY : MODE_ROWS;
   }
-  // f64 rows (NNP doubles per bin) are always streamed
+  // f64 rows (NNP doubles per bin) are streamed, but for N <= 512 (rows_res)
   int n_pad;
-  choose_bins(p->N, mode == MODE_POLY ? 8 : pl->mixed ? 4 : 0, pl->bpt, n_pad);
+  choose_bins(p->N, mode == MODE_POLY ? 8 : pl->mixed ? 4 : rows_res ? 2 : 0, pl->bpt, n_pad);
   // N in (2048, 4096] on an arithmetic depth grid: 16 bins per lane in the compact
   // layout (y, 1/uy, a in registers; c*x and t formed from the lane's first bin)
   double R16[24];
@@ -432,7 +437,7 @@ int plan_common(fitoct_plan* pl, const fitoct_problem* p, int chains, int precis
 }
 
 int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chains,
-                int force_bpt, fitoct_plan** out);
+                int force_bpt, fitoct_plan** out, bool poly_only = false);
 
 // Migrating tiles of several chains speculate once they host <= this many live chains.
 // Measured on config 3 at full length (profiles/r03_ab_spec_live.txt, two interleaved
@@ -704,7 +709,7 @@ int alloc_pairs(KParams& k, int tiles, int ppl, int** hdr, double** buf) {
 }
 
 int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chains,
-                int force_bpt, fitoct_plan** out) {
+                int force_bpt, fitoct_plan** out, bool poly_only) {
   if (!out) return fail(FITOCT_E_ARG, "out is NULL");
   *out = nullptr;
   if (!cfg) return fail(FITOCT_E_ARG, "config is NULL");
@@ -719,7 +724,7 @@ int plan_create(const fitoct_problem* prob, const fitoct_config* cfg, int g_chai
   std::unique_ptr<fitoct_plan, void (*)(fitoct_plan*)> guard(new fitoct_plan(), free_plan);
   fitoct_plan* pl = guard.get();
   int rc = plan_common(pl, prob, cfg->chains, cfg->precision, cfg->device, cfg->max_treedepth,
-                       g_chains, force_bpt);
+                       g_chains, force_bpt, poly_only);
   if (rc) return rc;
   pl->cfg = *cfg;
   KParams& k = pl->kp;
@@ -887,6 +892,7 @@ int32_t fitoct_plan_get_info(const fitoct_plan* pl, fitoct_plan_info* info) {
     info->ring_records_in_levels = 0;
     info->paired = pl->kp.pair;
     info->workgroups = pl->grid();
+    info->basis_mode = pl->kp.mode;
     return FITOCT_OK;
   });
 }
@@ -1130,6 +1136,17 @@ int32_t fitoct_plan_wait(fitoct_plan* pl) {
                   "for lookahead / record slot %.0f, in trees %.0f (leaves per tile %.0f)\n",
                   s, pe[s][0] / std::max(pe[s][2], 1.0), pe[s][1] / std::max(pe[s][2], 1.0),
                   pe[s][3] / std::max(pe[s][2], 1.0), pe[s][2] / pl->tiles);
+        for (int s = 0; s < 2; ++s) {
+          double q[4] = {0, 0, 0, 0}, n = 0;
+          for (int t = 0; t < pl->tiles; ++t) {
+            for (int k = 0; k < 4; ++k) q[k] += h[(size_t)NSTAMP * t + 100 + 4 * s + k];
+            n += h[(size_t)NSTAMP * t + 90 + 4 * s];
+          }
+          fprintf(stderr,
+                  "[fitoct stamps] producer of end %d per leaf (helped): finish_grad %.0f, stage %.0f, "
+                  "hand-over %.0f, prior_part %.0f\n", s, q[0] / std::max(n, 1.0),
+                  q[1] / std::max(n, 1.0), q[2] / std::max(n, 1.0), q[3] / std::max(n, 1.0));
+        }
         double hb2[2] = {0, 0}, hn2[2] = {0, 0};
         for (int t = 0; t < pl->tiles; ++t)
           for (int r = 0; r < 2; ++r) {
@@ -1302,6 +1319,9 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
     b->cfg.n_devices = 0;
     b->n_problems = n_problems;
     const int C = cfg->chains;
+    // one basis mode for the whole batch: resident rows only if every problem has N <= 512
+    bool poly_only = false;
+    for (int p = 0; p < n_problems; ++p) poly_only = poly_only || probs[p].N > 2 * GT;
     auto build = [&]() -> int {
       for (int p = 0; p < n_problems; ++p) {
         if (probs[p].prior_type != probs[0].prior_type || probs[p].Nn != probs[0].Nn)
@@ -1310,7 +1330,7 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
         fitoct_config c = b->cfg;
         c.chain_offset = cfg->chain_offset + p * C;
         fitoct_plan* pl = nullptr;
-        const int rc = plan_create(&probs[p], &c, n_problems * C, -1, &pl);
+        const int rc = plan_create(&probs[p], &c, n_problems * C, -1, &pl, poly_only);
         if (rc) return fail(rc, "problem " + std::to_string(p) + ": " + fitoct_last_error());
         b->plans.push_back(pl);
       }
@@ -1334,7 +1354,7 @@ int32_t fitoct_batch_create(const fitoct_problem* probs, int32_t n_problems,
           c.chain_offset = cfg->chain_offset + (int)p * C;
           free_plan(pl);
           b->plans[p] = nullptr;
-          const int rc = plan_create(&probs[p], &c, n_problems * C, to, &b->plans[p]);
+          const int rc = plan_create(&probs[p], &c, n_problems * C, to, &b->plans[p], poly_only);
           if (rc) return rc;
         }
         return FITOCT_OK;
@@ -1391,6 +1411,7 @@ int32_t fitoct_batch_get_info(const fitoct_batch* b, fitoct_plan_info* info) {
     info->tiles = b->tiles;
     info->paired = b->d_pair_hdr ? 1 : 0;
     info->workgroups = b->d_pair_hdr ? pair_grid(b->tiles) : b->tiles;
+    info->basis_mode = b->plans.empty() ? 0 : b->plans[0]->kp.mode;
     info->draws_bytes = (int64_t)(b->per_bytes * b->plans.size());
     return FITOCT_OK;
   });

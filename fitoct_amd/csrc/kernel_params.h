@@ -20,7 +20,7 @@ constexpr int NSLOT = 32;         // reduced sums per chain (4 + NNP <= 32)
 constexpr int MPW = 32;           // model-parameter words per chain (theta[3], pad, yGP[NNP])
 constexpr int POOL_VECS = 2;      // vectors per proposal-pool slot in HBM (q, grad)
 constexpr int KMAX = 24;          // max GP control points (K^-1 tile in LDS)
-constexpr int NSTAMP = 100;        // diagnostic stamps per tile (FITOCT_STAMPS)
+constexpr int NSTAMP = 108;        // diagnostic stamps per tile (FITOCT_STAMPS)
 constexpr int PAIR_HDR_INTS = 64; // paired tiles: hand-off words per pair (nuts_device.hip PairHdr)
 constexpr int PAIR_START_DOUBLES = 8;   // ... and per pair in pair_buf: the start's 4 vectors, then
                                         // these scalars, then the ring

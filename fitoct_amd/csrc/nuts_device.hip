@@ -3004,8 +3004,18 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nct = min(P.G, P.chains - c0);
   __shared__ unsigned long long ring[RINGN];
-  __shared__ int bd[BD_N];   // two-ended trajectories' hand-off words (BdWord)
+  __shared__ __attribute__((aligned(16))) int req_cnt[GMAX];   // sweeps posted per chain slot
   __shared__ int q_reserve, n_active, grad_cnt[GMAX];
+  // post a sweep of chain slot s (lane 0 of the posting wave; its MP writes are in before)
+  auto post_sweep = [&](const int s) {
+#if FITOCT_DOORBELL
+    __hip_atomic_fetch_add(&req_cnt[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+    const unsigned rs = (unsigned)atomicAdd(&q_reserve, 1);
+    __atomic_store_n(&ring[rs % RINGN], ((unsigned long long)rs << 32) | (unsigned)s, __ATOMIC_RELAXED);
+#endif
+  };
+  __shared__ int bd[BD_N];   // two-ended trajectories' hand-off words (BdWord)
   __shared__ long long done_t[GMAX];   // profiling build: when the 8th wave finished chain c
   __shared__ long long start_min[GMAX], start_max[GMAX];
   // speculative leaves (P.spec, tiles of one or two chains): chain slot c's NUTS wave posts
@@ -3078,6 +3088,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     start_max[tid] = 0;
   }
   if (tid < RINGN) ring[tid] = ~0ULL;
+  if (tid < GMAX) req_cnt[tid] = 0;
   // (a tile of one chain: the producers' areas are NUTS slots 1 and 2)
   if (tid < BD_N) bd[tid] = (tid == TW_SLOT) ? 1 : (tid == TW_SLOT + 1) ? 2 : 0;
   if (MIG && P.mig != nullptr) {   // every slot of the tile may host migrants: all NUTS waves live
@@ -3115,10 +3126,46 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     long long occ_t[GMAX + 1] = {0, 0, 0, 0, 0}, occ_n[GMAX + 1] = {0, 0, 0, 0, 0};
     long long occ_last = kProfile ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     int occ_k = GMAX;
+#ifndef FITOCT_SPIN
+#define FITOCT_SPIN 64
+#endif
+#if FITOCT_DOORBELL
+    // sweeps served per chain slot; the next slot to look at first (round robin)
+    int sv0 = 0, sv1 = 0, sv2 = 0, sv3 = 0, rr = 0;
+#endif
     for (unsigned h = 0;; ++h) {
       unsigned long long e;
       bool stop = false;
       Patience w;
+#if FITOCT_DOORBELL
+      int cdb = 0;
+      for (int np = 0;; np = min(np + 1, 64)) {  // wait for a posted sweep
+        const unsigned long long r01 = lds_load64((const unsigned long long*)&req_cnt[0]);
+        const unsigned long long r23 = lds_load64((const unsigned long long*)&req_cnt[2]);
+        const int m = ((int)(unsigned)r01 > sv0 ? 1 : 0) | ((int)(unsigned)(r01 >> 32) > sv1 ? 2 : 0) |
+                      ((int)(unsigned)r23 > sv2 ? 4 : 0) | ((int)(unsigned)(r23 >> 32) > sv3 ? 8 : 0);
+        if (m) {
+          const int rot = ((m >> rr) | (m << (4 - rr))) & 15;
+          cdb = (rr + __builtin_ctz(rot)) & 3;
+          break;
+        }
+        if (((np & 7) == 7 || np == 64) && lds_load(&n_active) == 0) {
+          stop = true;
+          break;
+        }
+        if (np < FITOCT_SPIN) continue;
+#elif FITOCT_POLL_FAST
+      // a wave that just finished a sweep spins on the ring (one LDS read per poll; the tile's
+      // end is checked every 8th poll) and sleeps only once the wait is long (an idle tile)
+      for (int np = 0;; np = min(np + 1, 64)) {  // wait for ring entry h
+        e = lds_load64(&ring[h % RINGN]);
+        if ((unsigned)(e >> 32) == h) break;
+        if (((np & 7) == 7 || np == 64) && lds_load(&n_active) == 0) {
+          stop = true;
+          break;
+        }
+        if (np < FITOCT_SPIN) continue;
+#else
       for (;;) {  // wait for ring entry h
         e = lds_load64(&ring[h % RINGN]);
         if ((unsigned)(e >> 32) == h) break;
@@ -3126,6 +3173,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           stop = true;
           break;
         }
+#endif
         // hang guard: with migration a tile may idle (receivers posted) until the launch's
         // last chain ends; without, its chains may pause between sweeps (a two-ended tree's
         // chain wave, init) but never for a leaf's wait bound
@@ -3136,7 +3184,17 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         __builtin_amdgcn_s_sleep(1);
       }
       if (stop) break;
+#if FITOCT_DOORBELL
+      const int c = __builtin_amdgcn_readfirstlane(cdb);
+      sv0 += c == 0;
+      sv1 += c == 1;
+      sv2 += c == 2;
+      sv3 += c == 3;
+      rr = (c + 1) & 3;
+      (void)e;
+#else
       const int c = (int)(e & 0xFF);
+#endif
       if (kProfile && wave == 0 && P.stamps != nullptr) {
         const long long now = (long long)__builtin_amdgcn_s_memrealtime();
         occ_t[occ_k] += now - occ_last;   // the interval since the last entry, at its count
@@ -3207,6 +3265,9 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       // profiling build: cycles waiting for sweeps, for the lookahead / ring room, leaves,
       // and cycles inside trees
       long long pf_sw = 0, pf_may = 0, pf_n = 0, pf_tree = 0;
+      // (and per leaf: finish_grad + end_update_p, staging the next leaf, the hand-over, prior_part)
+      long long pf_fg = 0, pf_st = 0, pf_ho = 0, pf_pp = 0;
+      auto pclk = [&]() -> long long { return kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0; };
       while (!quit) {
         int g;
         {
@@ -3318,11 +3379,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             q1.a[k] = fma(e, minv.a[k] * p1.a[k], qa.a[k]);
           }
           pr.write_mp(q1);
-          if (lane == 0) {
-            const unsigned rs = (unsigned)atomicAdd(&q_reserve, 1);
-            __atomic_store_n(&ring[rs % RINGN], ((unsigned long long)rs << 32) | (unsigned)slot,
-                             __ATOMIC_RELAXED);
-          }
+          if (lane == 0) post_sweep(slot);
           ++epoch;
         };
         int d = next_depth(-1);
@@ -3356,6 +3413,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             break;
           }
           wave_fence();
+          long long pc0 = pclk();
           // read with the partial sums (its latency hides in finish_grad's): a leaf the tree
           // no longer needs is dropped
           const int gen_now = lds_load(&bd[BD_GEN]);
@@ -3370,7 +3428,17 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           const bool last = j == (1 << d) - 1;
           const int dn = last ? next_depth(d) : d;
           const bool nxt = !last || (dn >= 0 && may(dn));
+          if (kProfile) {
+            const long long pc1 = pclk();
+            pf_fg += pc1 - pc0;
+            pc0 = pc1;
+          }
           if (nxt) stage(qn, pe, gn);
+          if (kProfile) {
+            const long long pc1 = pclk();
+            pf_st += pc1 - pc0;
+            pc0 = pc1;
+          }
           if (helped) {
             // hand this leaf to the booking helper (two slots: once it has booked the leaf
             // before the previous one); stop when a booking cut its subtree (nothing later on
@@ -3406,6 +3474,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             wave_publish();   // the leaf lands before its request number
             ++hreq;
             if (lane == 0) __atomic_store_n(&help_req[s], hreq, __ATOMIC_RELAXED);
+            if (kProfile) {
+              const long long pc1 = pclk();
+              pf_ho += pc1 - pc0;
+              pc0 = pc1;
+            }
             if (last) {
               if (dn < 0) break;   // this end has no further doubling in this tree
               if (!nxt) {
@@ -3418,6 +3491,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
               ++j;
             }
             pr.prior_part();
+            if (kProfile) pf_pp += pclk() - pc0;
             continue;
           }
           XF Tw{0.0, 0};
@@ -3455,6 +3529,11 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         o[1] = pf_may;
         o[2] = pf_n;
         o[3] = pf_tree;
+        AS_GLB long long* o2 = (AS_GLB long long*)P.stamps + (size_t)tix * NSTAMP + 100 + 4 * s;
+        o2[0] = pf_fg;
+        o2[1] = pf_st;
+        o2[2] = pf_ho;
+        o2[3] = pf_pp;
       }
     };
     // Two-ended trajectories in a tile of one chain: the booking helper (NUTS wave 1 of the tile,
@@ -3861,9 +3940,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
             continue;
           }
           if (lane == 0) {
-            const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
-            __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
-                             __ATOMIC_RELAXED);
+            post_sweep(c);
             if (ch.deep) {
               wave_publish();   // the hand-off (HX) lands before the request number
               __atomic_store_n(&help_req[c], hreq + 1, __ATOMIC_RELAXED);
@@ -3996,11 +4073,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if constexpr (kProfile) {
           if (P.bench_sweeps > 0 && P.stamps != nullptr) {   // sweep-only measurement
             for (int r = 0; r < P.bench_sweeps; ++r) {
-              if (lane == 0) {
-                const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
-                __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
-                                 __ATOMIC_RELAXED);
-              }
+              if (lane == 0) post_sweep(c);
               ++epoch;
               while (lds_load(&grad_cnt[c]) < (int)(NGW * epoch)) __builtin_amdgcn_s_sleep(1);
             }
@@ -4009,11 +4082,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           }
         }
         // enqueue chain c: sequence number from a ring-wide counter, one 64-bit store
-        if (lane == 0) {
-          const unsigned slot = (unsigned)atomicAdd(&q_reserve, 1);
-          __atomic_store_n(&ring[slot % RINGN], ((unsigned long long)slot << 32) | (unsigned)c,
-                           __ATOMIC_RELAXED);
-        }
+        if (lane == 0) post_sweep(c);
         if (stamp) t_enq = (long long)__builtin_amdgcn_s_memtime();
         ++epoch;
         // position-only work (prior terms, next merges' uniforms) overlaps the sweep
@@ -4196,6 +4265,11 @@ static hipError_t launch_n(bool logp, bool mixed, int bpt, const KParams& P, con
   if (!mixed) {
     if (P.mode == MODE_POLY)
       return launch_m<double, NNP, PPL, MODE_POLY>(logp, bpt, P, dP, tiles, st, tm);
+    if constexpr (NNP == 15 && PPL == 1) {   // N <= 512: the rows in registers
+      if (bpt == 1) return launch_t<double, 1, NNP, PPL, MODE_ROWS>(logp, P, dP, tiles, st, tm);
+      if (bpt == 2) return launch_t<double, 2, NNP, PPL, MODE_ROWS>(logp, P, dP, tiles, st, tm);
+    }
+    if (bpt != 0) return hipErrorInvalidValue;
     return launch_t<double, 0, NNP, PPL, MODE_ROWS>(logp, P, dP, tiles, st, tm);
   }
   return launch_m<float, NNP, PPL, MODE_ROWS>(logp, bpt, P, dP, tiles, st, tm);

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FITOCT_ABI_VERSION 7
+#define FITOCT_ABI_VERSION 8
 /* largest accepted N (depth bins): bounds every host and device allocation derived from it */
 #define FITOCT_MAX_BINS (1 << 22)
 /* largest device list of one call (fitoct_config.devices) */
@@ -182,6 +182,11 @@ typedef struct fitoct_plan_info {
    * tile to grow both ends itself (fitoct_result::paired_transitions counts the paired ones). */
   int32_t paired;
   int32_t workgroups;      /* workgroups launched (tiles, or 16 * ceil(tiles / 8) when paired) */
+  /* ABI 8: how the sweep forms the GP modulation.  0: the factorised basis (per-bin
+   * polynomial, K^-1 products in the sampler's leaf); 1: the basis rows B[i, :] (resident in
+   * the gradient waves' registers for N <= 512 -- bins_per_thread 1 or 2 -- or streamed for
+   * a caller's basis).  The struct's size is unchanged (the slot was padding). */
+  int32_t basis_mode;
 } fitoct_plan_info;
 
 /* fitoct_plan_info::sampler.  PLAIN: no speculation, no migration;

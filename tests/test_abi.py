@@ -46,7 +46,7 @@ def test_struct_layouts_match_ctypes():
     sizes = _lib.struct_sizes()
     assert sizes == (C.sizeof(_lib.Problem), C.sizeof(_lib.Config), C.sizeof(_lib.Result),
                      C.sizeof(_lib.PlanInfo))
-    assert _lib.lib().fitoct_abi_version() == 7 == _lib.ABI_VERSION
+    assert _lib.lib().fitoct_abi_version() == 8 == _lib.ABI_VERSION
 
 
 def test_default_config_is_stan_default():

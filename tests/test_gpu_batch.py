@@ -90,3 +90,18 @@ def test_batch_rejects_mixed_models():
     probs = [_prob(300, "sincExp", 1), _prob(300, "sincExp", 2, family="lasso")]
     with pytest.raises(FitOCTError, match="share prior_type and Nn"):
         Batch(probs, SamplerConfig(chains=2, warmup=10, samples=10))
+
+
+def test_basis_mode_rows_resident_up_to_512_bins():
+    """N <= 512 (configs 2 and 5): the sweep reads the basis rows from registers (basis_mode
+    1, 1-2 bins of 15 doubles per lane) and the sampler's leaf has no K^-1 products; wider
+    problems use the factorised basis (basis_mode 0).  A batch takes one mode for all its
+    problems: rows only if every problem has N <= 512 (`fitoct_plan_info::basis_mode`)."""
+    cfg = SamplerConfig(chains=4, warmup=10, samples=10, seed=2, max_treedepth=5)
+    for N, mode, bpt in ((481, 1, 2), (200, 1, 1), (512, 1, 2), (700, 0, 4), (2048, 0, 8)):
+        with Plan(_prob(N, "sincExp", 7), cfg) as pl:
+            assert (pl.info["basis_mode"], pl.info["bins_per_thread"]) == (mode, bpt), N
+    with Batch([_prob(481, "sincExp", 1), _prob(200, "sincExp1", 2)], cfg) as b:
+        assert (b.info["basis_mode"], b.info["bins_per_thread"]) == (1, 2)
+    with Batch([_prob(481, "sincExp", 1), _prob(700, "sincExp1", 2)], cfg) as b:
+        assert (b.info["basis_mode"], b.info["bins_per_thread"]) == (0, 4)

@@ -43,16 +43,17 @@ LAUNCHED = [
     ("config 3 without speculation (FITOCT_NO_SPEC)", 2, mangled(8, 2, True, False), 63),
     ("config 4: lasso N=4096, 16 bins per lane, migrating + tail speculation",
      1, mangled(16, 1, True, True), 150),
+    # N <= 512: the basis rows resident in the gradient waves (MODE_ROWS = 1, 2 bins per lane)
     ("config 2: normal N=512, 128 chains, paired tiles of one chain (two-ended trajectories)",
-     0, mangled(2, 0, False, True, True), 96),
+     0, mangled(2, 0, False, True, True, mode=1), 96),
     ("config 2 unpaired (FITOCT_NO_PAIR; 129..256 one-chain tiles)", 0,
-     mangled(2, 0, False, True), 147),
+     mangled(2, 0, False, True, mode=1), 147),
     ("config 5 at one GPU: batch tiles of four chains, plain sampler", 0,
-     mangled(2, 0, False, False), 45),
+     mangled(2, 0, False, False, mode=1), 47),
     ("config 5 8-GPU share: paired batch tiles of one chain", 0,
-     mangled(2, 0, False, True, True), 96),
+     mangled(2, 0, False, True, True, mode=1), 96),
     ("config 5 4-GPU share: batch tiles of one chain (speculating)", 0,
-     mangled(2, 0, False, True), 147),
+     mangled(2, 0, False, True, mode=1), 147),
 ]
 
 
@@ -128,4 +129,13 @@ def test_every_resident_bin_instantiation_keeps_the_chain_in_registers(fam):
             else:
                 assert r.get("VGPRs Spill", -1) == 0 and r.get("ScratchSize", -1) == 0, (k, r)
             seen += 1
-    assert seen == 25
+    # N <= 512: the resident basis rows (MODE_ROWS, 1-2 bins of 15 doubles per lane)
+    for bpt in (1, 2):
+        for mig, spec, pair in ((False, False, False), (False, True, False), (False, True, True),
+                                (True, False, False), (True, True, False)):
+            k = mangled(bpt, fam, mig, spec, pair, mode=1)
+            assert k in rows, k
+            r = rows[k]
+            assert r.get("VGPRs Spill", -1) == 0 and r.get("ScratchSize", -1) == 0, (k, r)
+            seen += 1
+    assert seen == 35
