@@ -1042,7 +1042,8 @@ struct Vd {
 // run: one chain per tile, batch mode, FITOCT_NO_MIGRATE), so the receive loop
 // and the donor check cost no registers in the NUTS waves
 // SPEC = true: speculative leaves with a helper wave (one chain per tile, no migration)
-template <int PPL, int NNP, int FAM, bool MIG = true, bool SPEC = false>
+// MODE_: the kernel's basis mode (MODE_POLY / MODE_ROWS) as a constant, or -1: read P.mode
+template <int PPL, int NNP, int FAM, bool MIG = true, bool SPEC = false, int MODE_ = -1>
 struct Chain {
   using V = Vd<PPL>;
   static constexpr int VLEN = WAVE * PPL;
@@ -1059,7 +1060,7 @@ struct Chain {
   // this lane's row of K^-1 (lanes < NNP) held in VGPRs for the two K^-1 matvecs
   // of every leaf (write_mp, finish_grad): same arithmetic, no LDS reads on the
   // NUTS wave's critical path (configs 2 / 5 +2 %).  Not at NNP = 24 (it would spill).
-  static constexpr bool KROW = NNP <= 16 && !MIG;
+  static constexpr bool KROW = NNP <= 16 && !MIG && MODE_ != MODE_ROWS;
   // fexp's Horner steps as three-VGPR FMAs (fma_v) in the non-migrating samplers: bitwise
   // the same, configs 2 / 5 +2 / +0.6 %.  The migrating samplers then spill a VGPR (the
   // headline horseshoe one loses 2.2 %, profiles/r03_ab_fmav.txt): they keep the compiler's form
@@ -1131,6 +1132,9 @@ struct Chain {
   }
 
   __device__ __forceinline__ KPc& Pr() const { return *pp; }
+  __device__ __forceinline__ bool is_poly() const {
+    return MODE_ >= 0 ? MODE_ == MODE_POLY : Pr().mode == MODE_POLY;
+  }
   // two-ended trajectories: producer k's chain area (NUTS slot bd[TW_SLOT + k] of this
   // tile: the chain areas are consecutive, chain_bytes apart), its scalars and vectors
   __device__ __forceinline__ AS_LDS char* parea(int k) const {
@@ -1228,7 +1232,7 @@ struct Chain {
     FITOCT_MARK(write_mp);
     long long ts = stamp0();
     const int Nn = Pr().Nn, D = Pr().D;
-    const bool poly = Pr().mode == MODE_POLY;
+    const bool poly = is_poly();
     AS_LDS double* qs = vec(V_QS);
     AS_LDS double* qe = vec(V_QE);
 #pragma unroll
@@ -1398,12 +1402,29 @@ struct Chain {
   __device__ double finish_grad(V& g, double& s0) const {
     FITOCT_MARK(finish_grad);
     const int Nn = Pr().Nn, D = Pr().D;
-    const bool lik = (Pr().prior_PD == 0), poly = Pr().mode == MODE_POLY;
+    const bool lik = (Pr().prior_PD == 0), poly = is_poly();
     const V pg = ld(V_PG), ca = ld(V_CA);   // issued up front, used last
     const double pr_lp = Sp->pr_lp, pr_is2 = Sp->pr_is2;
     const double fw = (FAM == FAM_HORSESHOE && lane < Nn) ? AUX[64 + lane] : 0.0;
     double famsum = 0.0, S0 = 0.0;
-    if (lik) {
+    double srow[PPL];   // basis rows (MODE_ROWS): the bin sum each lane's gradient needs
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) srow[s] = 0.0;
+    if (lik && !poly) {
+      // each lane sums the partials of the sums it needs itself, in the SUMS path's order
+      // (bitwise the same values): no store / wait / read-back before the gradient
+      const AS_LDS double* pw = part + slot * NGW * NSLOT;
+      double v = 0.0;
+      const int jv = lane < NNP ? 4 + lane : 0;
+#pragma unroll
+      for (int w = 0; w < NGW; ++w) {
+        S0 += pw[w * NSLOT];
+        if (FAM == FAM_HORSESHOE) v += pw[w * NSLOT + jv];
+#pragma unroll
+        for (int s = 0; s < PPL; ++s) srow[s] += pw[w * NSLOT + sidx(idx(s))];
+      }
+      if (FAM == FAM_HORSESHOE) famsum = wave_sum(lane < Nn ? fw * v : 0.0);
+    } else if (lik) {
       double sl = 0.0;
       if (lane < 4 + NNP) {
 #pragma unroll
@@ -1437,7 +1458,7 @@ struct Chain {
       const int k = idx(s);
       double gk = pg.a[s];
       if (lik && k < D) {
-        gk = fma(ca.a[s], SUMS[sidx(k)], gk);
+        gk = fma(ca.a[s], poly ? SUMS[sidx(k)] : srow[s], gk);
         if (FAM == FAM_HORSESHOE && (k == 3 + Nn || k == 4 + Nn))
           gk = fma(k == 3 + Nn ? 1.0 : 0.5, famsum, gk);
       }
@@ -2982,6 +3003,10 @@ __device__ int receive_chain(KPc& P, const Lds<PPL>& L, int c, int lane, volatil
 template <class R, int BPT, int NNP, int PPL, int MODE, int FAM, bool MIG, bool SPEC, bool PAIR>
 __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict__ Pg,
                                                       const int* __restrict__ tile_map) {
+  // the basis mode as a constant of the sampler's chain code (config 5 at one GPU +3 %), but
+  // for the speculating row-mode samplers, which read it (config 2 +1.7 %: the compiler's
+  // schedule of the producers; same-box A/B, profiles/r06_ab_rows.txt)
+  constexpr int CMODE = (SPEC && MODE == MODE_ROWS) ? -1 : MODE;
   int tix = blockIdx.x, role = 0;
   if constexpr (PAIR) {
     role = (tix >> 3) & 1;
@@ -3004,16 +3029,13 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nct = min(P.G, P.chains - c0);
   __shared__ unsigned long long ring[RINGN];
-  __shared__ __attribute__((aligned(16))) int req_cnt[GMAX];   // sweeps posted per chain slot
   __shared__ int q_reserve, n_active, grad_cnt[GMAX];
-  // post a sweep of chain slot s (lane 0 of the posting wave; its MP writes are in before)
+  // post a sweep of chain slot s (lane 0 of the posting wave; its MP writes are in before):
+  // sequence number from a ring-wide counter, one 64-bit store.  (Per-slot doorbells without
+  // the atomic's return measured -7 %, profiles/r06_ab_rows.txt.)
   auto post_sweep = [&](const int s) {
-#if FITOCT_DOORBELL
-    __hip_atomic_fetch_add(&req_cnt[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
     const unsigned rs = (unsigned)atomicAdd(&q_reserve, 1);
     __atomic_store_n(&ring[rs % RINGN], ((unsigned long long)rs << 32) | (unsigned)s, __ATOMIC_RELAXED);
-#endif
   };
   __shared__ int bd[BD_N];   // two-ended trajectories' hand-off words (BdWord)
   __shared__ long long done_t[GMAX];   // profiling build: when the 8th wave finished chain c
@@ -3026,7 +3048,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       help_dead[2];
   const bool spec = SPEC;
   const bool helped = SPEC && !MIG && P.G <= 2;   // spare NUTS waves help the tile's chains
-  const bool bidi = Chain<PPL, NNP, FAM, MIG, SPEC>::kTwoEnded && helped &&
+  const bool bidi = Chain<PPL, NNP, FAM, MIG, SPEC, CMODE>::kTwoEnded && helped &&
                    P.bidi != 0;   // ... and two producer waves
   __shared__ int live_chains;   // chains the tile hosts (speculation policy, Chain::live)
   // paired tiles: this pair's hand-off words and buffer; pair_on: the partner has joined
@@ -3088,7 +3110,6 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     start_max[tid] = 0;
   }
   if (tid < RINGN) ring[tid] = ~0ULL;
-  if (tid < GMAX) req_cnt[tid] = 0;
   // (a tile of one chain: the producers' areas are NUTS slots 1 and 2)
   if (tid < BD_N) bd[tid] = (tid == TW_SLOT) ? 1 : (tid == TW_SLOT + 1) ? 2 : 0;
   if (MIG && P.mig != nullptr) {   // every slot of the tile may host migrants: all NUTS waves live
@@ -3126,46 +3147,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     long long occ_t[GMAX + 1] = {0, 0, 0, 0, 0}, occ_n[GMAX + 1] = {0, 0, 0, 0, 0};
     long long occ_last = kProfile ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     int occ_k = GMAX;
-#ifndef FITOCT_SPIN
-#define FITOCT_SPIN 64
-#endif
-#if FITOCT_DOORBELL
-    // sweeps served per chain slot; the next slot to look at first (round robin)
-    int sv0 = 0, sv1 = 0, sv2 = 0, sv3 = 0, rr = 0;
-#endif
     for (unsigned h = 0;; ++h) {
       unsigned long long e;
       bool stop = false;
       Patience w;
-#if FITOCT_DOORBELL
-      int cdb = 0;
-      for (int np = 0;; np = min(np + 1, 64)) {  // wait for a posted sweep
-        const unsigned long long r01 = lds_load64((const unsigned long long*)&req_cnt[0]);
-        const unsigned long long r23 = lds_load64((const unsigned long long*)&req_cnt[2]);
-        const int m = ((int)(unsigned)r01 > sv0 ? 1 : 0) | ((int)(unsigned)(r01 >> 32) > sv1 ? 2 : 0) |
-                      ((int)(unsigned)r23 > sv2 ? 4 : 0) | ((int)(unsigned)(r23 >> 32) > sv3 ? 8 : 0);
-        if (m) {
-          const int rot = ((m >> rr) | (m << (4 - rr))) & 15;
-          cdb = (rr + __builtin_ctz(rot)) & 3;
-          break;
-        }
-        if (((np & 7) == 7 || np == 64) && lds_load(&n_active) == 0) {
-          stop = true;
-          break;
-        }
-        if (np < FITOCT_SPIN) continue;
-#elif FITOCT_POLL_FAST
-      // a wave that just finished a sweep spins on the ring (one LDS read per poll; the tile's
-      // end is checked every 8th poll) and sleeps only once the wait is long (an idle tile)
-      for (int np = 0;; np = min(np + 1, 64)) {  // wait for ring entry h
-        e = lds_load64(&ring[h % RINGN]);
-        if ((unsigned)(e >> 32) == h) break;
-        if (((np & 7) == 7 || np == 64) && lds_load(&n_active) == 0) {
-          stop = true;
-          break;
-        }
-        if (np < FITOCT_SPIN) continue;
-#else
       for (;;) {  // wait for ring entry h
         e = lds_load64(&ring[h % RINGN]);
         if ((unsigned)(e >> 32) == h) break;
@@ -3173,7 +3158,6 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
           stop = true;
           break;
         }
-#endif
         // hang guard: with migration a tile may idle (receivers posted) until the launch's
         // last chain ends; without, its chains may pause between sweeps (a two-ended tree's
         // chain wave, init) but never for a leaf's wait bound
@@ -3184,17 +3168,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         __builtin_amdgcn_s_sleep(1);
       }
       if (stop) break;
-#if FITOCT_DOORBELL
-      const int c = __builtin_amdgcn_readfirstlane(cdb);
-      sv0 += c == 0;
-      sv1 += c == 1;
-      sv2 += c == 2;
-      sv3 += c == 3;
-      rr = (c + 1) & 3;
-      (void)e;
-#else
       const int c = (int)(e & 0xFF);
-#endif
       if (kProfile && wave == 0 && P.stamps != nullptr) {
         const long long now = (long long)__builtin_amdgcn_s_memrealtime();
         occ_t[occ_k] += now - occ_last;   // the interval since the last entry, at its count
@@ -3242,7 +3216,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     __builtin_amdgcn_s_setprio(3);
     const int c = wave - NGW;
     const bool mig = MIG && P.mig != nullptr;
-    using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
+    using Ch = Chain<PPL, NNP, FAM, MIG, SPEC, CMODE>;
     // Two-ended trajectories: producer of trajectory end s (0: backward, 1: forward) on NUTS
     // slot `slot` (its chain area holds the end's state, its subtree's levels and merge
     // uniforms, and its last subtree's record; its proposal pool is its own).  For every
@@ -3866,7 +3840,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       if (lane == 0) atomicAdd(&bd[BD_EXIT], 1);
     }
     if (helped && !bidi && c >= P.G && c - P.G < nct) {   // the helper wave of chain slot c - G
-      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
+      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC, CMODE>;
       const int hs = c - P.G;
       Ch ch(P, L, hs, c0 + hs, lane, nct);
       int seen = 0;
@@ -3896,7 +3870,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
       }
     }
     if (role == 0 && c < (mig ? P.G : nct)) {
-      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC>;
+      using Ch = Chain<PPL, NNP, FAM, MIG, SPEC, CMODE>;
       long long epoch = 0;     // this slot's hand-offs (grad_cnt[c] counts NGW per epoch)
       int lc = c < nct ? c0 + c : -1;
       int a = Ch::A_INIT_STATE;
