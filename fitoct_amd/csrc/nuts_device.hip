@@ -3032,7 +3032,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
   __shared__ int q_reserve, n_active, grad_cnt[GMAX];
   // post a sweep of chain slot s (lane 0 of the posting wave; its MP writes are in before):
   // sequence number from a ring-wide counter, one 64-bit store.  (Per-slot doorbells without
-  // the atomic's return measured -7 %, profiles/r06_ab_rows.txt.)
+  // the atomic's return measured -3 to -6 %, gradient waves at priority 2-3 during sweeps
+  // -16 to -19 % on config 2: profiles/r06_ab_rows.txt.)
   auto post_sweep = [&](const int s) {
     const unsigned rs = (unsigned)atomicAdd(&q_reserve, 1);
     __atomic_store_n(&ring[rs % RINGN], ((unsigned long long)rs << 32) | (unsigned)s, __ATOMIC_RELAXED);
