@@ -732,13 +732,16 @@ __device__ __forceinline__ void moments_geo_add(KPc& P, double t0, const double 
 }
 
 // MODE_ROWS / MODE_STREAM: dL = B_i . yGP ; (B^T h)_k += B_ik h
-template <class R, int NNP, class A>
+// LAT (f64, 1-2 bins per lane: a latency-bound sweep): exp by Estrin's scheme (config 5 at
+// one GPU +7 %, config 2 +-0; the dot product in three FMA chains as well measured config 5
+// +10 % but config 2 -1.8 %, alone config 5 -8 %: profiles/r06_ab_rows.txt)
+template <class R, int NNP, class A, bool LAT = false>
 __device__ __forceinline__ void bin_rows(R cx, R y, R isu, const R (&Brow)[NNP], R th1, R th2,
                                          R th3, const R (&yg)[NNP], A (&acc)[4 + NNP], R& umin) {
   R dL = R(0);
 #pragma unroll
   for (int k = 0; k < NNP; ++k) dL = fma(Brow[k], yg[k], dL);
-  const R h = bin_core<R, A, 4 + NNP>(R(1) + dL, cx, y, isu, th1, th2, th3, acc, umin);
+  const R h = bin_core<R, A, 4 + NNP, LAT>(R(1) + dL, cx, y, isu, th1, th2, th3, acc, umin);
 #pragma unroll
   for (int k = 0; k < NNP; ++k) acc[4 + k] = fma((A)Brow[k], (A)h, acc[4 + k]);
 }
@@ -917,7 +920,9 @@ struct Lds {
 
 // The likelihood sweep of chains [cb, ce) of the tile (gradient waves only).
 // PART[c][wave][0 .. 4+NNP) receives this wave's partial sums of chain c.
-template <class R, int BPT, int NNP, int MODE>
+// LATR: the row-mode sweep's latency form (bin_rows LAT); every sampler and the logp kernel
+// use it, so all paths keep computing the same gradient bit for bit.
+template <class R, int BPT, int NNP, int MODE, bool LATR = false>
 __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                               const AS_LDS double* mpall, AS_LDS double* part, const int* done,
                               int cb, int ce,
@@ -993,13 +998,14 @@ __device__ void gradient_pass(KPc& P, const Bins<R, BPT, NNP, MODE>& bins,
                                  bins.row[b][1], th1, th2, th3, cf, acc, umin);
     } else if constexpr (BPT > 0) {
       // the few bins of one lane accumulate in R, the lane totals in f64
+      constexpr bool ROWS_LAT = LATR && sizeof(R) == 8 && BPT <= 2;
       R racc[4 + NNP];
 #pragma unroll
       for (int k = 0; k < 4 + NNP; ++k) racc[k] = R(0);
 #pragma unroll
       for (int b = 0; b < BPT; ++b)
-        bin_rows<R, NNP, R>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b], th1, th2, th3, cf,
-                            racc, umin);
+        bin_rows<R, NNP, R, ROWS_LAT>(bins.cx[b], bins.y[b], bins.isu[b], bins.row[b], th1, th2,
+                                      th3, cf, racc, umin);
 #pragma unroll
       for (int k = 0; k < 4 + NNP; ++k) acc[k] = (double)racc[k];
     } else {
@@ -3185,8 +3191,8 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         atomicMax((unsigned long long*)&start_max[c], t);
       }
       if (P.prior_PD == 0)
-        gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1, tid,
-                                         lane, wave);
+        gradient_pass<R, BPT, NNP, MODE, true>(P, bins, L.mp(0), L.part(), zero_done, c, c + 1,
+                                               tid, lane, wave);
       wave_publish();   // this wave's PART writes before its count
       if (wstamp) t_wbusy += (long long)__builtin_amdgcn_s_memtime() - s0w;
       if (lane == 0) {
@@ -4146,7 +4152,8 @@ __global__ void __launch_bounds__(TPB, 2) logp_kernel(const KParams* __restrict_
   if (wave < NGW && P.prior_PD == 0) {
     Bins<R, BPT, NNP, MODE> bins;
     bins.load(P, tid);
-    gradient_pass<R, BPT, NNP, MODE>(P, bins, L.mp(0), L.part(), done, 0, nct, tid, lane, wave);
+    gradient_pass<R, BPT, NNP, MODE, true>(P, bins, L.mp(0), L.part(), done, 0, nct, tid, lane,
+                                           wave);
   }
   __syncthreads();
   if (wave >= NGW && c < nct) {
