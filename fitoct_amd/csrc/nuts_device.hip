@@ -2100,7 +2100,8 @@ struct Chain {
   // ERR_TIMEOUT if a producer's record never came (a fault)
   // profiling build: this wave's cycles waiting for records / booking, subtrees booked
   long long pf_wait = 0, pf_busy = 0, pf_n = 0;
-  __device__ __forceinline__ int bidi_book_tree(const int g) {
+  template <class Idle>
+  __device__ __forceinline__ int bidi_book_tree(const int g, Idle&& idle) {
     const uint32_t t = (uint32_t)uni(Sp->t);
     const V minv = ld(V_MINV);
     int m0 = 0, m1 = 0;
@@ -2118,7 +2119,7 @@ struct Chain {
           lost = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        if (!idle()) __builtin_amdgcn_s_sleep(1);
       }
       if (lost) {
         Sp->status = ERR_TIMEOUT;
@@ -3010,9 +3011,9 @@ template <class R, int BPT, int NNP, int PPL, int MODE, int FAM, bool MIG, bool 
 __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict__ Pg,
                                                       const int* __restrict__ tile_map) {
   // the basis mode as a constant of the sampler's chain code (config 5 at one GPU +3 %), but
-  // for the speculating row-mode samplers, which read it (config 2 +1.7 %: the compiler's
-  // schedule of the producers; same-box A/B, profiles/r06_ab_rows.txt)
-  constexpr int CMODE = (SPEC && MODE == MODE_ROWS) ? -1 : MODE;
+  // for the paired row-mode sampler, which reads it (config 2 +1.7 %: the compiler's schedule
+  // of the producers; same-box A/B, profiles/r06_ab_rows.txt)
+  constexpr int CMODE = (SPEC && PAIR && MODE == MODE_ROWS) ? -1 : MODE;
   int tix = blockIdx.x, role = 0;
   if constexpr (PAIR) {
     role = (tix >> 3) & 1;
@@ -3233,10 +3234,12 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     // previous one.  `epoch`: the slot's sweeps so far (grad_cnt[slot] counts NGW per sweep).
     // Ends with BD_GEN < 0 (the tile's chain finished) or, in a migrating tile, with the launch.
     auto produce = [&](const int s, const int slot, long long epoch) {
-      // helped: a helper wave books this end's leaves (serve: tiles of one chain -- the backward
-      // end, and in a paired launch the forward end too), else the producer books them itself
-      // (the forward end in an unpaired tile, a migrating launch's tail)
-      const bool helped = !MIG && (s == 0 || PAIR);
+      // helped: another wave books this end's leaves (serve: tiles of one chain -- the backward
+      // end the booking helper; the forward end the partner tile's helper, or in an unpaired
+      // row-mode tile the chain's wave while it waits for records), else the producer books them
+      // itself (an unpaired tile with the factorised basis, whose registers have no room for the
+      // chain's serving; a migrating launch's tail)
+      const bool helped = !MIG && (s == 0 || PAIR || MODE == MODE_ROWS);
       int hreq = 0;   // leaves handed to the helper
       Ch pr(P, L, slot, c0, lane, nct);
       pr.bd = (volatile AS_LDS int*)bd;
@@ -3524,7 +3527,10 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
     // one after.  One request of producer s: 1 served, 0 none pending, -1 the producer is gone.
     // (help_seen / help_gen / help_m: requests served, and the transition and records published
     // of producer s, kept by the helper.)
-    auto serve = [&](const int s) -> int {
+    // nb (the chain's wave serving the forward end of an unpaired tile): serve a leaf only if its
+    // subtree's record would find its slot free -- that wave alone frees the slots, so it must
+    // never wait for one here.  0 then: not served (the request stays pending).
+    auto serve = [&](const int s, const bool nb) -> int {
       const int rq0 = lds_load(&help_req[s]);
       if (rq0 < 0) return -1;
       const int rq = lds_load(&help_seen[s]) + 1;   // requests are served in order
@@ -3552,6 +3558,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         hc.key = make_key(P.seed, (uint32_t)(P.chain_offset + lds_load(&bd[TW_LC])));
         int hm = lds_load(&help_m[s]);
         if (lds_load(&help_gen[s]) != gen) hm = 0;
+        if (nb && lds_load(&bd[BD_CONS + s]) < hm - Ch::RSLOTS + 1) return 0;
         if (j == 0) hc.sub_begin(d);
         XF Tw{0.0, 0};
         int Tprop = -1;
@@ -3811,7 +3818,7 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         long long pf_busy = 0, pf_n = 0;   // profiling build: cycles booking, leaves booked
         for (int s = role;; s = (both && role == 0) ? s ^ 1 : s) {   // (one call site of serve)
           const long long pt = kProfile ? (long long)__builtin_amdgcn_s_memtime() : 0;
-          const int a = serve(s);
+          const int a = serve(s, false);
           if (a > 0) {
             if (kProfile) {
               pf_busy += (long long)__builtin_amdgcn_s_memtime() - pt;
@@ -3897,7 +3904,12 @@ __global__ void __launch_bounds__(TPB, 2) nuts_kernel(const KParams* __restrict_
         if (Ch::kTwoEnded && y == Ch::A_BIDI_TREE) {   // the producers grow the subtrees
           const int g = lds_load(&bd[BD_GEN]);
           const bool late = false;
-          ch.bidi_book_tree(g);   // this wave books the trajectory level
+          // this wave books the trajectory level; in an unpaired tile it books the forward end's
+          // leaves too while it waits for records
+          ch.bidi_book_tree(g, [&]() -> bool {
+            if constexpr (!PAIR && !MIG && MODE == MODE_ROWS) return serve(1, true) > 0;
+            return false;
+          });
           wave_publish();   // the producers stop growing this tree
           if (lane == 0) {
             __atomic_store_n(&bd[BD_GEN], g | BD_ENDED, __ATOMIC_RELAXED);
