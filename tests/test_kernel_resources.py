@@ -49,13 +49,13 @@ LAUNCHED = [
     ("config 2: normal N=512, 128 chains, paired tiles of one chain (two-ended trajectories)",
      0, mangled(2, 0, False, True, True, mode=1), 103),
     ("config 2 unpaired (FITOCT_NO_PAIR; 129..256 one-chain tiles)", 0,
-     mangled(2, 0, False, True, mode=1), 152),
+     mangled(2, 0, False, True, mode=1), 76),
     ("config 5 at one GPU: batch tiles of four chains, plain sampler", 0,
      mangled(2, 0, False, False, mode=1), 36),
     ("config 5 8-GPU share: paired batch tiles of one chain", 0,
      mangled(2, 0, False, True, True, mode=1), 103),
     ("config 5 4-GPU share: batch tiles of one chain (speculating)", 0,
-     mangled(2, 0, False, True, mode=1), 152),
+     mangled(2, 0, False, True, mode=1), 76),
 ]
 
 
