@@ -691,7 +691,12 @@ namespace {
 // A partner that does not get a CU at launch leaves its primary to grow both ends (the pair's
 // hand-shake), so this is safe on a shared GPU too.  FITOCT_NO_PAIR=1: off.
 bool want_pairs(const KParams& k, int tiles, int ncu) {
-  return k.bidi && k.G == 1 && pair_grid(tiles) <= ncu && getenv("FITOCT_NO_PAIR") == nullptr;
+  if (!(k.bidi && k.G == 1 && pair_grid(tiles) <= ncu) || getenv("FITOCT_NO_PAIR") != nullptr)
+    return false;
+  // with the basis rows (N <= 512) an unpaired tile is faster (its chain's wave books the
+  // forward end: config 2 253 k vs 245 k draws/s, profiles/r06_ab_unpaired.txt), so there the
+  // pairing is on only with FITOCT_PAIR=1
+  return k.mode == MODE_POLY || getenv("FITOCT_PAIR") != nullptr;
 }
 // the pairs' hand-off words and buffers for `tiles` tiles; sets every k.pair_* but the count
 int alloc_pairs(KParams& k, int tiles, int ppl, int** hdr, double** buf) {

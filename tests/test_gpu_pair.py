@@ -23,7 +23,7 @@ from test_gpu_sampler import _prob
 
 pytestmark = pytest.mark.gpu
 
-ENV = ("FITOCT_NO_PAIR", "FITOCT_NO_BIDI", "FITOCT_TEST_PAIR_ABSENT", "FITOCT_NO_SPEC")
+ENV = ("FITOCT_PAIR", "FITOCT_NO_PAIR", "FITOCT_NO_BIDI", "FITOCT_TEST_PAIR_ABSENT", "FITOCT_NO_SPEC")
 
 
 def _with_env(env, fn):
@@ -66,7 +66,7 @@ def _same(a, b):
 def test_paired_tiles_preserve_draws_bitwise(family, N, chains, depth):
     prob = _prob(family, N, 15)
     cfg = SamplerConfig(chains=chains, warmup=80, samples=60, seed=41, max_treedepth=depth)
-    info, a = _plan_run(prob, cfg)
+    info, a = _plan_run(prob, cfg, FITOCT_PAIR="1")   # (row mode pairs only on request)
     i1, b = _plan_run(prob, cfg, FITOCT_NO_PAIR="1")
     i2, c = _plan_run(prob, cfg, FITOCT_NO_BIDI="1")
     assert info["chains_per_tile"] == 1 and info["two_ended"] == 1 and info["paired"] == 1
@@ -89,7 +89,7 @@ def test_absent_partners_leave_the_primary_to_grow_both_ends():
     paired transition."""
     prob = _prob("normal", 512, 15)
     cfg = SamplerConfig(chains=64, warmup=60, samples=40, seed=43, max_treedepth=8)
-    info, a = _plan_run(prob, cfg, FITOCT_TEST_PAIR_ABSENT="1")
+    info, a = _plan_run(prob, cfg, FITOCT_TEST_PAIR_ABSENT="1", FITOCT_PAIR="1")
     _, b = _plan_run(prob, cfg, FITOCT_NO_PAIR="1")
     assert info["paired"] == 1
     assert a.paired_transitions == 0 and a.two_ended_transitions > 0
@@ -106,7 +106,7 @@ def test_batch_of_one_chain_tiles_pairs_bitwise():
         with Batch(probs, cfg) as b:
             b.run()
             return b.info, [b.download(p) for p in range(len(probs))]
-    ia, a = _with_env({}, go)
+    ia, a = _with_env({"FITOCT_PAIR": "1"}, go)
     ib, b = _with_env({"FITOCT_NO_PAIR": "1"}, go)
     assert ia["chains_per_tile"] == 1 and ia["paired"] == 1 and ib["paired"] == 0
     assert ia["workgroups"] == 256 and ib["workgroups"] == 128
@@ -123,3 +123,16 @@ def test_pairs_off_where_twice_the_tiles_do_not_fit():
     info, a = _plan_run(prob, cfg)
     assert info["chains_per_tile"] == 1 and info["two_ended"] == 1
     assert info["paired"] == 0 and a.paired_transitions == 0
+
+
+def test_pairing_default_follows_the_basis_mode():
+    """By default one-chain tiles pair only with the factorised basis (N > 512): with the basis
+    rows (N <= 512) an unpaired tile, whose chain's wave books the forward end, is faster
+    (config 2: 253 k vs 245 k draws/s, profiles/r06_ab_unpaired.txt); FITOCT_PAIR=1 pairs it."""
+    cfg = SamplerConfig(chains=16, warmup=10, samples=10, seed=3, max_treedepth=6)
+    info, _ = _plan_run(_prob("normal", 512, 15), cfg)
+    assert info["basis_mode"] == 1 and info["two_ended"] == 1 and info["paired"] == 0
+    info, _ = _plan_run(_prob("normal", 512, 15), cfg, FITOCT_PAIR="1")
+    assert info["paired"] == 1
+    info, _ = _plan_run(_prob("horseshoe", 2048, 15), cfg)
+    assert info["basis_mode"] == 0 and info["paired"] == 1

@@ -46,15 +46,15 @@ LAUNCHED = [
     ("config 4: lasso N=4096, 16 bins per lane, migrating + tail speculation",
      1, mangled(16, 1, True, True), 138),
     # N <= 512: the basis rows resident in the gradient waves (MODE_ROWS = 1, 2 bins per lane)
-    ("config 2: normal N=512, 128 chains, paired tiles of one chain (two-ended trajectories)",
+    ("config 2 paired (FITOCT_PAIR: normal N=512, 128 chains, partner tiles)",
      0, mangled(2, 0, False, True, True, mode=1), 103),
-    ("config 2 unpaired (FITOCT_NO_PAIR; 129..256 one-chain tiles)", 0,
+    ("config 2: one-chain tiles, two-ended, unpaired (row mode; 129..256 chains too)", 0,
      mangled(2, 0, False, True, mode=1), 76),
     ("config 5 at one GPU: batch tiles of four chains, plain sampler", 0,
      mangled(2, 0, False, False, mode=1), 36),
-    ("config 5 8-GPU share: paired batch tiles of one chain", 0,
+    ("config 5 8-GPU share with FITOCT_PAIR: paired batch tiles of one chain", 0,
      mangled(2, 0, False, True, True, mode=1), 103),
-    ("config 5 4-GPU share: batch tiles of one chain (speculating)", 0,
+    ("config 5 4- and 8-GPU shares: batch tiles of one chain (two-ended)", 0,
      mangled(2, 0, False, True, mode=1), 76),
 ]
 
